@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Benchmark: batched acrobot Newton/Armijo swing-up on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_PER_GPU]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One *step* = one complete batched solve (newton_Algorithm semantics per lane, task-2 settings:
+tol 1e-4, gamma_0 0.1, beta 0.7, c 0.5, <= 20 Armijo trials, max_iters 5000) of this rank's shard
+of synthetic lanes, from u = 0 to every lane converged / failed, with inputs resident in HBM.
+Workload (N=1): BASELINE cfg 3 -- 262,144 lanes per GPU, x0 = [th1, th2, 0, 0], th ~ U(-0.5,0.5)
+(numpy default_rng(0)), lane 0 = 0 (the golden lane), T = 500 stages, fp64.  Weak scaling: every GPU
+owns 262,144 lanes; ranks exchange one 64-byte all-reduce per outer iteration.
+
+value = lane-iterations executed by all ranks / max-over-ranks wall time  ("Newton iterations/s";
+states/s = value * T).  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "swing-up Newton iterations/sec (batch×T states/s) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
+
+
+def algorithmic_bytes(N: int) -> dict:
+    """Compulsory HBM bytes per lane per launch (fp64), see DESIGN.md section 4.
+
+    backward: read x (4N) + u (2T); write K row 1 (4T) + sigma (2T)      (K row 0 == 0 is not stored)
+    trial   : read x (4T... the whole x is needed for dx, 4N) + u (2T) + K1 (4T) + sigma (2T);
+              write x_new (4N) + u_new (2T)
+    """
+    T = N - 1
+    return {"backward": 8 * (4 * N + 2 * T + 4 * T + 2 * T),
+            "trial": 8 * (4 * N + 2 * T + 4 * T + 2 * T + 4 * N + 2 * T),
+            "survey_per_iteration": 8 * ((4 * N + 2 * T) + 10 * T + (2 * (4 * N + 2 * T) + 10 * T))}
+
+
+def load_refs():
+    d = np.load(os.path.join(ROOT, "gymnast_optimalcontrol_amd", "data", "fully_actuated_trajectory.npz"))
+    u_ref = np.zeros(d["u"].shape)
+    u_ref[:, 1] = d["u"][:, 1]
+    return d["x"], 2.0 * u_ref          # get_fully_actuated_ref (trajectory_generation.py:511-518)
+
+
+def make_x0(total: int, seed: int = 0) -> np.ndarray:
+    x0 = np.zeros((total, 4))
+    x0[:, :2] = np.random.default_rng(seed).uniform(-0.5, 0.5, (total, 2))
+    x0[0] = 0.0                          # golden lane (main.task_2, main.py:55)
+    return x0
+
+
+def cpu_baseline(x0, x_ref, u_ref, lanes: int, max_iters: int):
+    """The plain-C oracle (OpenMP over lanes) on a bounded sample of the same workload."""
+    from oracle import c_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    c_oracle.lib()
+    t0 = time.perf_counter()
+    r = c_oracle.newton_solve(x0[:lanes], x_ref, u_ref, max_iters=max_iters, tol=1e-4, gamma_0=0.1)
+    dt = time.perf_counter() - t0
+    its = int(r["n_iter"].sum())
+    return {"value": its / dt, "unit": "Newton iterations/s", "cores": threads, "kind": "port",
+            "sample": f"first {lanes} lanes of the bench workload solved to convergence ({its} lane-iterations, "
+                      f"{dt:.1f} s) by oracle/acrobot_oracle.c (fp64, OpenMP {threads} threads)",
+            "seconds": dt, "lane_iterations": its}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=262144, help="lanes per GPU (weak scaling)")
+    ap.add_argument("--max-iters", type=int, default=5000)
+    ap.add_argument("--cpu-lanes", type=int, default=512)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
+    a = ap.parse_args()
+
+    import torch
+    from gymnast_optimalcontrol_amd import distributed as gd
+    rank, local_rank, world = gd.init_process_group()
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+
+    x_ref, u_ref = load_refs()
+    N = x_ref.shape[0]
+    T = N - 1
+    total = a.batch * world
+    x0_all = make_x0(total)
+    lo, hi = gd.shard_range(total, rank, world)
+    eng = AcrobotEngine()
+    solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20)
+    if not a.no_timing:
+        solver.enable_timing()
+    x0_dev = eng.t(x0_all[lo:hi])                  # inputs resident in HBM before the timed region
+    reduce = gd.make_reduce_stats()
+
+    for _ in range(a.warmup):
+        solver.solve(x0_dev, a.max_iters, reduce_stats=reduce)
+    solver.reset_timing()
+    gd.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lane_its = 0
+    res = None
+    for _ in range(a.steps):
+        res = solver.solve(x0_dev, a.max_iters, reduce_stats=reduce)
+        lane_its += res.lane_iterations
+    torch.cuda.synchronize()
+    gd.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = gd.max_over_ranks(elapsed)
+    lane_its_all = int(gd.sum_over_ranks(lane_its))
+    kt = solver.kernel_times()
+    n_iters_outer = res.iterations
+
+    # parity of the golden lane (rank 0 owns lane 0)
+    parity = None
+    if rank == 0:
+        g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))
+        x0l, u0l = res.x[0].cpu().numpy(), res.u[0].cpu().numpy()
+        st = res.status.cpu().numpy()
+        parity = {"lane0_rel_l2_x": float(np.linalg.norm(x0l - g["x"]) / np.linalg.norm(g["x"])),
+                  "lane0_rel_l2_u": float(np.linalg.norm(u0l - g["u"]) / np.linalg.norm(g["u"])),
+                  "lane0_iters": int(res.n_iter[0].item()), "tolerance": 1e-8,
+                  "converged_frac": float((st == 1).mean()), "ls_failed": int((st == 2).sum()),
+                  "outer_iterations": int(n_iters_outer),
+                  "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())]}
+
+    value = lane_its_all / elapsed
+    out = {"metric": METRIC, "value": value, "unit": "Newton iterations/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"cfg3: {a.batch} randomised-theta0 acrobot swing-ups per GPU, T={T}, fp64, "
+                                  "task-2 Newton/Armijo settings, solved to convergence",
+                      "lanes_per_gpu": a.batch, "global_lanes": total, "horizon_T": T,
+                      "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats / iteration)"},
+           "states_per_s": value * T}
+
+    if kt and rank == 0:
+        ab = algorithmic_bytes(N)
+        kern = {}
+        for kind, (ms, launches) in kt.items():
+            if launches:
+                kern[kind] = {"avg_ms": ms / launches, "launches": launches}
+        # lanes processed per launch: every lane runs the backward sweep and trial 1 each iteration it is active
+        lane_launch = lane_its / max(1, kt["trial"][1]) if kt["trial"][1] else 0
+        for kind in ("backward", "trial"):
+            if kind in kern:
+                by = ab[kind] * lane_launch
+                kern[kind]["algorithmic_bytes_per_launch"] = by
+                kern[kind]["achieved_GBs"] = by / (kern[kind]["avg_ms"] * 1e-3) / 1e9
+        dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):
+            try:
+                traffic = json.load(open(tfile)).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        ach = kern[dom]["achieved_GBs"]
+        out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                           "bytes_per_lane": ab[dom], "lanes_per_launch": lane_launch}
+        out["kernels"] = kern
+    if parity is not None:
+        out["parity"] = parity
+    if rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(x0_all, x_ref, u_ref, a.cpu_lanes, a.max_iters)
+        out["cpu_baseline"]["reference_python_single_core"] = {
+            "value": 5.0, "unit": "Newton iterations/s", "note": "reference newton_Algorithm, 1 core, build "
+            "container (Intel Xeon), SURVEY.md 3.1: 0.199 s/iteration; not a same-box measurement"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

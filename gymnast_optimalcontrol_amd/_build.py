@@ -1,0 +1,54 @@
+"""Build the in-tree HIP library ``libgymnast_acrobot.so`` for gfx950 (MI355X).
+
+    python -m gymnast_optimalcontrol_amd._build          # or __graft_entry__.build()
+
+hipcc cross-compiles without a GPU.  The .so is git-ignored but travels to the GPU box with
+the working tree.  Nothing here ever falls back to a CPU implementation.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIB_NAME = "libgymnast_acrobot.so"
+LIB_PATH = os.path.join(PKG, LIB_NAME)
+SOURCES = [os.path.join(CSRC, "acrobot_kernels.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, "acrobot_device.hpp"), os.path.join(INCLUDE, "gymnast_acrobot.h")]
+ARCH = os.environ.get("GYM_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the HIP library)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

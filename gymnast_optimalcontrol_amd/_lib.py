@@ -1,0 +1,131 @@
+"""ctypes binding of the C-ABI in include/gymnast_acrobot.h (libgymnast_acrobot.so).
+
+The HIP library is the only compute path of this package.  If it is missing, or no HIP
+device is visible, every compute entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so the library binds to the same one
+
+from . import _build
+
+LIB_PATH = _build.LIB_PATH
+
+# exported symbols, in include/gymnast_acrobot.h order (tests check every one is present)
+EXPORTS = (
+    "gym_abi_version", "gym_model_from_params",
+    "gym_continuous_dynamics", "gym_rk4_step", "gym_jacobians", "gym_stage_cost_derivs",
+    "gym_pack_lanes", "gym_unpack_lanes", "gym_unpack_gains",
+    "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
+    "gym_riccati_general",
+    "gym_newton_init", "gym_newton_iteration", "gym_newton_finalize",
+    "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
+)
+KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats")
+
+ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4
+STATUS_NAMES = {ACTIVE: "active", CONVERGED: "converged", LS_FAILED: "ls_failed", MAX_ITERS: "max_iters", PAD: "pad"}
+
+
+class GymModel(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("a", "b", "d", "g1", "g2", "f1", "f2", "dt")]
+
+
+class GymWeights(C.Structure):
+    _fields_ = [("Q", C.c_double * 4), ("R", C.c_double * 2), ("QT", C.c_double * 4)]
+
+
+class GymArmijo(C.Structure):
+    _fields_ = [("tol", C.c_double), ("beta", C.c_double), ("c", C.c_double), ("gamma0", C.c_double),
+                ("max_ls", C.c_int32), ("record_history", C.c_int32)]
+
+
+_P = C.c_void_p
+
+
+class GymTiming(C.Structure):
+    _fields_ = [("ev", _P * 10), ("ms", C.c_double * 5), ("launches", C.c_int64 * 5), ("pending", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class GymBatch(C.Structure):
+    _fields_ = [("B", C.c_int64), ("Bp", C.c_int64), ("N", C.c_int32), ("hist_len", C.c_int32),
+                ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("sigma", _P), ("x_ref", _P), ("u_ref", _P),
+                ("cost", _P), ("dJ", _P), ("smax", _P), ("gamma", _P), ("status", _P), ("n_iter", _P),
+                ("res_buf", _P), ("n_roll", _P), ("retry_list", _P), ("counters", _P), ("cand_ok", _P),
+                ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P),
+                ("timing", C.POINTER(GymTiming))]
+
+
+_I64, _I32, _D = C.c_int64, C.c_int32, C.c_double
+_MP, _WP, _AP, _BP = C.POINTER(GymModel), C.POINTER(GymWeights), C.POINTER(GymArmijo), C.POINTER(GymBatch)
+_SIGS = {
+    "gym_abi_version": [],
+    "gym_model_from_params": [_P, _D, _MP],
+    "gym_continuous_dynamics": [_MP, _P, _P, _P, _I64, _P],
+    "gym_rk4_step": [_MP, _P, _P, _P, _I64, _P],
+    "gym_jacobians": [_MP, _P, _P, _P, _P, _I64, _P],
+    "gym_stage_cost_derivs": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _P],
+    "gym_pack_lanes": [_P, _P, _I64, _I64, _I32, _I32, _P],
+    "gym_unpack_lanes": [_P, _P, _P, _P, _I64, _I64, _I32, _I32, _P],
+    "gym_unpack_gains": [_P, _P, _I64, _I64, _I32, _P],
+    "gym_rollout_open_loop": [_MP, _WP, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_closed_loop": [_MP, _WP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_total_cost": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_backward_sweep": [_MP, _WP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_linearize": [_MP, _WP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_riccati_general": [_P] * 12 + [_I64, _I64, _I32, _P],
+    "gym_newton_init": [_MP, _WP, _P, _BP, _P],
+    "gym_newton_iteration": [_MP, _WP, _AP, _BP, _I32, _P],
+    "gym_newton_finalize": [_BP, _I32, _P, _P, _P, _P, _P],
+    "gym_timing_create": [C.POINTER(GymTiming)],
+    "gym_timing_destroy": [C.POINTER(GymTiming)],
+    "gym_timing_collect": [C.POINTER(GymTiming)],
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library.  Raises if the HIP library is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ImportError(
+                f"{path} is missing: build the HIP library first (python -m gymnast_optimalcontrol_amd._build "
+                "or __graft_entry__.build()); there is no CPU fallback")
+        lib = C.CDLL(path)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")
+
+
+def require_device(device=None) -> torch.device:
+    """The compute path runs on a HIP device only."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("gymnast_optimalcontrol_amd needs a HIP (ROCm) GPU: no device is visible "
+                           "and there is no CPU fallback")
+    load()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"device must be a HIP device, got {dev}")
+    return dev
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

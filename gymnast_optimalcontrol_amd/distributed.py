@@ -1,0 +1,99 @@
+"""Lane sharding across GPUs: one process per GPU, torch.distributed over RCCL (backend "nccl").
+
+Trajectories are independent, so the batch is partitioned into contiguous shards with no
+data-path collective.  The only exchange is one SUM all-reduce per outer iteration of the 8
+solver statistics (solver.STAT_FIELDS: active lanes, sum of J, sum of max|sigma|^2, ...), which
+gives every rank the global stop condition and the global cost / descent-norm scalars.  The
+message is 64 bytes, so it is latency-bound; it is issued on the solver's stream.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced [lo, hi) lane range of ``rank`` (first ``total % world`` ranks get one more)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, extra = divmod(int(total), world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def env_rank_world() -> tuple[int, int, int]:
+    """(rank, local_rank, world_size) from torchrun's environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_process_group(backend: str | None = None):
+    """Initialise torch.distributed from the environment if WORLD_SIZE > 1 (RCCL on GPUs, gloo on CPU)."""
+    rank, local_rank, world = env_rank_world()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {"device_id": torch.device("cuda", local_rank)} if backend == "nccl" else {}
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    return rank, local_rank, world
+
+
+def make_reduce_stats(group=None):
+    """SUM all-reduce of the per-iteration statistics, or None when running a single process."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return None
+    backend = dist.get_backend(group)
+
+    def reduce_stats(st):
+        if isinstance(st, np.ndarray):
+            st = torch.from_numpy(st.copy())
+        t = st.detach().cpu().clone() if backend == "gloo" else st.detach().clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return t
+
+    return reduce_stats
+
+
+def barrier(group=None):
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier(group=group)
+
+
+def max_over_ranks(value: float, group=None) -> float:
+    """Max of a host scalar over ranks (timing: the job's time is its slowest rank's)."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def sum_over_ranks(value: float, group=None) -> float:
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t.item())
+
+
+def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, **solver_kw):
+    """Solve this rank's contiguous shard of ``x0_all`` (B_total,4); stop on the GLOBAL active count.
+
+    Returns (lo, hi, SolveResult of the local shard)."""
+    from .engine import AcrobotEngine
+    from .solver import BatchedNewtonSolver
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    lo, hi = shard_range(len(x0_all), rank, world)
+    eng = engine or AcrobotEngine()
+    solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **solver_kw)
+    res = solver.solve(np.asarray(x0_all)[lo:hi], max_iters, reduce_stats=make_reduce_stats())
+    return lo, hi, res

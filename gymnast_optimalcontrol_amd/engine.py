@@ -1,0 +1,287 @@
+"""Batched tensor-level front end of the HIP engine (device tensors in, device tensors out).
+
+Every method is a thin launcher over one C-ABI entry point of include/gymnast_acrobot.h; the
+arithmetic runs in the gfx950 kernels of csrc/acrobot_kernels.hip.  Inputs are fp64 tensors
+(any device / numpy are copied to the engine's HIP device); outputs stay on the device.
+
+Lane-major shapes follow the reference stacked over lanes: x (B,N,4), u (B,T,2), K (B,T,2,4),
+sigma (B,T,2).  Internally trajectories live in the SoA "pairs" layout (see the header).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import PARAM_SETS, DT, Q_DIAG, R_DIAG, QT_DIAG
+
+F64 = torch.float64
+
+
+def padded(B: int) -> int:
+    return max(64, (B + 63) // 64 * 64)
+
+
+@dataclass
+class Weights:
+    Q: tuple = Q_DIAG
+    R: tuple = R_DIAG
+    QT: tuple = QT_DIAG
+
+    def c_struct(self) -> _lib.GymWeights:
+        w = _lib.GymWeights()
+        w.Q[:] = [float(v) for v in self.Q]
+        w.R[:] = [float(v) for v in self.R]
+        w.QT[:] = [float(v) for v in self.QT]
+        return w
+
+    @staticmethod
+    def from_matrices(Q, R, QT) -> "Weights":
+        """Diagonal weights from the reference's matrices; raises if they are not diagonal."""
+        out = []
+        for name, M, n in (("Q", Q, 4), ("R", R, 2), ("Q_T", QT, 4)):
+            M = np.asarray(M, dtype=float)
+            if M.shape != (n, n):
+                raise ValueError(f"{name} must be {n}x{n}, got {M.shape}")
+            if np.any(M - np.diag(np.diag(M))):
+                raise NotImplementedError(f"the fused solver kernels take diagonal {name}; use the generic path")
+            out.append(tuple(np.diag(M)))
+        return Weights(*out)
+
+
+class AcrobotEngine:
+    """Launchers for one acrobot parameter set on one HIP device."""
+
+    def __init__(self, params=1, dt: float = DT, weights: Weights | None = None, device=None):
+        self.device = _lib.require_device(device)
+        self.lib = _lib.load()
+        p = PARAM_SETS[params] if isinstance(params, int) else params
+        self.params = dict(p)
+        self.dt = float(dt)
+        self.model = _lib.GymModel()
+        vec = np.array([p[k] for k in ("m1", "m2", "l1", "lc1", "l2", "lc2", "I1", "I2", "g", "f1", "f2")], float)
+        _lib.check(self.lib.gym_model_from_params(vec.ctypes.data, self.dt, C.byref(self.model)),
+                   "gym_model_from_params")
+        self.weights = weights or Weights()
+        self._w = self.weights.c_struct()
+
+    # -------------------------------------------------------------------------------- utils
+    def t(self, a, shape=None) -> torch.Tensor:
+        """fp64 contiguous tensor on the engine device."""
+        if isinstance(a, torch.Tensor):
+            out = a.to(device=self.device, dtype=F64)
+        else:
+            out = torch.as_tensor(np.asarray(a, dtype=np.float64), device=self.device)
+        if shape is not None:
+            out = out.reshape(shape)
+        return out.contiguous()
+
+    @property
+    def stream(self) -> int:
+        return _lib.stream_handle(self.device)
+
+    def set_weights(self, weights: Weights):
+        self.weights = weights
+        self._w = weights.c_struct()
+
+    def pack(self, a: torch.Tensor, Bp: int) -> torch.Tensor:
+        """(B,L,C) lane-major -> SoA (L, C/2, Bp, 2)."""
+        B, L, Cc = a.shape
+        out = torch.empty((L, Cc // 2, Bp, 2), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_pack_lanes(a.data_ptr(), out.data_ptr(), B, Bp, L, Cc, self.stream),
+                   "gym_pack_lanes")
+        return out
+
+    def unpack(self, soa: torch.Tensor, B: int, soa1: torch.Tensor | None = None,
+               sel: torch.Tensor | None = None) -> torch.Tensor:
+        L, P, Bp, _ = soa.shape
+        out = torch.empty((B, L, 2 * P), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_unpack_lanes(soa.data_ptr(), _lib.ptr(soa1), _lib.ptr(sel), out.data_ptr(), B, Bp,
+                                             L, 2 * P, self.stream), "gym_unpack_lanes")
+        return out
+
+    def refs(self, x_ref, u_ref):
+        x_ref = self.t(x_ref)
+        u_ref = self.t(u_ref)
+        if x_ref.ndim != 2 or x_ref.shape[1] != 4:
+            raise ValueError(f"x_ref must be (N,4), got {tuple(x_ref.shape)}")
+        if u_ref.shape[0] == x_ref.shape[0]:        # trajectory_generation.py:301-303
+            u_ref = u_ref[:-1].contiguous()
+        if u_ref.ndim != 2 or u_ref.shape[1] != 2 or u_ref.shape[0] != x_ref.shape[0] - 1:
+            raise ValueError(f"Incompatible dimensions: x_ref has {x_ref.shape[0]} states but u_ref has "
+                             f"{u_ref.shape[0]} controls (expected {x_ref.shape[0] - 1})")
+        return x_ref, u_ref
+
+    # --------------------------------------------------------------------- point primitives
+    def _points(self, x, u):
+        x = self.t(x); u = self.t(u)
+        n = x.numel() // 4
+        return x.reshape(n, 4), u.reshape(n, 2), n
+
+    def continuous_dynamics(self, x, u) -> torch.Tensor:
+        x, u, n = self._points(x, u)
+        out = torch.empty((n, 4), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_continuous_dynamics(C.byref(self.model), x.data_ptr(), u.data_ptr(), out.data_ptr(),
+                                                    n, self.stream), "gym_continuous_dynamics")
+        return out
+
+    def rk4(self, x, u) -> torch.Tensor:
+        x, u, n = self._points(x, u)
+        out = torch.empty((n, 4), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_rk4_step(C.byref(self.model), x.data_ptr(), u.data_ptr(), out.data_ptr(), n,
+                                         self.stream), "gym_rk4_step")
+        return out
+
+    def jacobians(self, x, u):
+        x, u, n = self._points(x, u)
+        A = torch.empty((n, 4, 4), dtype=F64, device=self.device)
+        Bm = torch.empty((n, 4, 2), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_jacobians(C.byref(self.model), x.data_ptr(), u.data_ptr(), A.data_ptr(),
+                                          Bm.data_ptr(), n, self.stream), "gym_jacobians")
+        return A, Bm
+
+    def stage_cost_derivs(self, x, x_ref, u, u_ref, Q, R, terminal=False):
+        x = self.t(x).reshape(-1, 4); xr = self.t(x_ref).reshape(-1, 4)
+        n = x.shape[0]
+        Qm = np.ascontiguousarray(np.asarray(Q, float).reshape(4, 4))
+        l = torch.empty(n, dtype=F64, device=self.device)
+        gx = torch.empty((n, 4), dtype=F64, device=self.device)
+        if terminal:
+            u_ = ur_ = gu = None
+            Rm = None
+        else:
+            u_ = self.t(u).reshape(-1, 2); ur_ = self.t(u_ref).reshape(-1, 2)
+            Rm = np.ascontiguousarray(np.asarray(R, float).reshape(2, 2))
+            gu = torch.empty((n, 2), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_stage_cost_derivs(
+            x.data_ptr(), xr.data_ptr(), _lib.ptr(u_), _lib.ptr(ur_), Qm.ctypes.data,
+            None if Rm is None else Rm.ctypes.data, int(bool(terminal)), l.data_ptr(), gx.data_ptr(), _lib.ptr(gu),
+            n, self.stream), "gym_stage_cost_derivs")
+        return l, gx, gu
+
+    # ----------------------------------------------------------------- trajectory kernels
+    def rollout_open_loop(self, x0, u, x_ref, u_ref):
+        """simulate_open_loop (+ total_cost): x0 (B,4), u (B,T,2) -> x (B,N,4), J (B,)."""
+        x0 = self.t(x0).reshape(-1, 4)
+        B = x0.shape[0]
+        x_ref, u_ref = self.refs(x_ref, u_ref)
+        N = x_ref.shape[0]
+        u = self.t(u)
+        if u.ndim == 2:
+            u = u.expand(B, -1, -1).contiguous()
+        if u.shape != (B, N - 1, 2):
+            raise ValueError(f"u must be ({B},{N - 1},2), got {tuple(u.shape)}")
+        Bp = padded(B)
+        us = self.pack(u, Bp)
+        xs = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device)
+        J = torch.empty(Bp, dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_rollout_open_loop(C.byref(self.model), C.byref(self._w), x0.data_ptr(),
+                                                  us.data_ptr(), x_ref.data_ptr(), u_ref.data_ptr(), xs.data_ptr(),
+                                                  J.data_ptr(), B, Bp, N, self.stream), "gym_rollout_open_loop")
+        return self.unpack(xs, B), J[:B]
+
+    def closed_loop(self, x, u, K, sigma, gamma, x_ref, u_ref):
+        """forward_closed_loop_update (+ total_cost of the result), full gains K (B,T,2,4)."""
+        x = self.t(x); u = self.t(u); K = self.t(K); sigma = self.t(sigma)
+        B, N, _ = x.shape
+        T = N - 1
+        x_ref, u_ref = self.refs(x_ref, u_ref)
+        Bp = padded(B)
+        g = torch.zeros(Bp, dtype=F64, device=self.device)
+        g[:B] = self.t(gamma).reshape(-1).expand(B) if self.t(gamma).numel() == 1 else self.t(gamma).reshape(B)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        Ks = self.pack(K.reshape(B, T, 8), Bp)
+        ss = self.pack(sigma, Bp)
+        xn = torch.empty_like(xs); un = torch.empty_like(us)
+        J = torch.empty(Bp, dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_closed_loop(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),
+                                            Ks.data_ptr(), ss.data_ptr(), g.data_ptr(), x_ref.data_ptr(),
+                                            u_ref.data_ptr(), xn.data_ptr(), un.data_ptr(), J.data_ptr(), B, Bp, N,
+                                            self.stream), "gym_closed_loop")
+        return self.unpack(xn, B), self.unpack(un, B), J[:B]
+
+    def total_cost(self, x, u, x_ref, u_ref, Q, R, QT):
+        x = self.t(x); u = self.t(u)
+        B, N, _ = x.shape
+        x_ref = self.t(x_ref); u_ref = self.t(u_ref)[: N - 1].contiguous()
+        Bp = padded(B)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        mats = [np.ascontiguousarray(np.asarray(M, float)) for M in (Q, R, QT)]
+        J = torch.empty(Bp, dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_total_cost(xs.data_ptr(), us.data_ptr(), x_ref.data_ptr(), u_ref.data_ptr(),
+                                           mats[0].ctypes.data, mats[1].ctypes.data, mats[2].ctypes.data,
+                                           J.data_ptr(), B, Bp, N, self.stream), "gym_total_cost")
+        return J[:B]
+
+    def backward(self, x, u, x_ref, u_ref, want_lambda=False):
+        """Fused costate + stage lists + Riccati: K (B,T,2,4), sigma (B,T,2), dJ (B,), max|sigma| (B,), lambda."""
+        x = self.t(x); u = self.t(u)
+        B, N, _ = x.shape
+        T = N - 1
+        x_ref, u_ref = self.refs(x_ref, u_ref)
+        Bp = padded(B)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        K1 = torch.empty((T, 2, Bp, 2), dtype=F64, device=self.device)
+        sg = torch.empty((T, 1, Bp, 2), dtype=F64, device=self.device)
+        dJ = torch.empty(Bp, dtype=F64, device=self.device)
+        sm = torch.empty(Bp, dtype=F64, device=self.device)
+        lam = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device) if want_lambda else None
+        _lib.check(self.lib.gym_backward_sweep(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),
+                                               x_ref.data_ptr(), u_ref.data_ptr(), K1.data_ptr(), sg.data_ptr(),
+                                               dJ.data_ptr(), sm.data_ptr(), _lib.ptr(lam), B, Bp, N, self.stream),
+                   "gym_backward_sweep")
+        K = torch.empty((B, T, 2, 4), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_unpack_gains(K1.data_ptr(), K.data_ptr(), B, Bp, T, self.stream), "gym_unpack_gains")
+        return K, self.unpack(sg, B), dJ[:B], sm[:B], (self.unpack(lam, B) if want_lambda else None)
+
+    def linearize(self, x, u, x_ref, u_ref):
+        """build_stage_lists: A_d (B,T,4,4), B_d (B,T,4,2), q (B,T,4), r (B,T,2), q_T (B,4)."""
+        x = self.t(x); u = self.t(u)
+        B, N, _ = x.shape
+        T = N - 1
+        x_ref, u_ref = self.refs(x_ref, u_ref)
+        Bp = padded(B)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        e = lambda *s: torch.empty(s, dtype=F64, device=self.device)  # noqa: E731
+        Ad, Bd, q, r, qT = e(T, 16, Bp), e(T, 8, Bp), e(T, 4, Bp), e(T, 2, Bp), e(4, Bp)
+        _lib.check(self.lib.gym_linearize(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),
+                                          x_ref.data_ptr(), u_ref.data_ptr(), Ad.data_ptr(), Bd.data_ptr(),
+                                          q.data_ptr(), r.data_ptr(), qT.data_ptr(), B, Bp, N, self.stream),
+                   "gym_linearize")
+        lm = lambda a, *s: a[..., :B].permute(-1, *range(a.ndim - 1)).reshape(B, *s)  # noqa: E731
+        return lm(Ad, T, 4, 4), lm(Bd, T, 4, 2), lm(q, T, 4), lm(r, T, 2), lm(qT, 4)
+
+    def riccati_general(self, A, Bm, Q, R, S, q, r, QT, qT):
+        """calculate_K_and_sigma on dense per-lane stage data (lane-major, broadcastable over lanes/time)."""
+        A = self.t(A)
+        B, T = A.shape[:2]
+        Bp = padded(B)
+
+        def soa(a, shape_tail):  # (B,T,*tail) or broadcastable -> (T, prod(tail), Bp)
+            a = self.t(a).expand(B, T, *shape_tail) if a is not None else None
+            n = int(np.prod(shape_tail))
+            out = torch.zeros((T, n, Bp), dtype=F64, device=self.device)
+            out[:, :, :B] = a.reshape(B, T, n).permute(1, 2, 0)
+            return out
+
+        def soa_t(a, shape_tail):
+            a = self.t(a).expand(B, *shape_tail)
+            n = int(np.prod(shape_tail))
+            out = torch.zeros((n, Bp), dtype=F64, device=self.device)
+            out[:, :B] = a.reshape(B, n).T
+            return out
+
+        As, Bs, Qs, Rs, Ss = soa(A, (4, 4)), soa(Bm, (4, 2)), soa(Q, (4, 4)), soa(R, (2, 2)), soa(S, (2, 4))
+        qs, rs, QTs, qTs = soa(q, (4,)), soa(r, (2,)), soa_t(QT, (4, 4)), soa_t(qT, (4,))
+        K = torch.empty((T, 8, Bp), dtype=F64, device=self.device)
+        sg = torch.empty((T, 2, Bp), dtype=F64, device=self.device)
+        dJ = torch.empty(Bp, dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_riccati_general(As.data_ptr(), Bs.data_ptr(), Qs.data_ptr(), Rs.data_ptr(),
+                                                Ss.data_ptr(), qs.data_ptr(), rs.data_ptr(), QTs.data_ptr(),
+                                                qTs.data_ptr(), K.data_ptr(), sg.data_ptr(), dJ.data_ptr(), B, Bp, T,
+                                                self.stream), "gym_riccati_general")
+        return (K[..., :B].permute(2, 0, 1).reshape(B, T, 2, 4), sg[..., :B].permute(2, 0, 1).contiguous(),
+                dJ[:B])

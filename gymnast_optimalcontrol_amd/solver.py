@@ -1,0 +1,222 @@
+"""Batched Newton / Armijo swing-up solver on the HIP engine (newton_Algorithm, batched).
+
+Reference semantics, per lane (trajectory_generation.py:298-398):
+  * u_ref trimmed to N-1 rows if it has N (:301-303); ValueError on other mismatches (:305-306);
+  * u_0 = 0 and x_0 = open-loop rollout (:311-312); J_0 = total_cost (:319);
+  * each iteration: backward sweep -> K, sigma, dJ (:332-338); Armijo gamma_0, gamma_0*beta, ...
+    with the strict test J_new < J + c*gamma*dJ (:352-365), at most ``max_ls`` = 20 trials;
+  * LS failure: stop without update (:367-369); otherwise update, then stop if max|sigma| < tol
+    (:383-396).
+The batch runs every lane in lock-step on the device.  Trial 1 is fused with its rollout; lanes
+that reject it evaluate trials 2..max_ls *in parallel* (one thread per candidate) and re-run the
+first accepted one -- the same decision the sequential search makes.
+
+Multi-GPU: one process per GPU, each owning a contiguous shard of lanes; the only cross-GPU
+traffic is one all-reduce (SUM) of the 8 per-iteration statistics (see distributed.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import AcrobotEngine, padded, F64
+from .params import MAX_LINE_SEARCH_ITERS
+
+STAT_FIELDS = ("n_active", "sum_cost", "sum_smax2", "lanes_ran", "n_retry", "n_converged", "n_failed", "n_rollouts")
+
+
+@dataclass
+class SolveResult:
+    x: torch.Tensor          # (B,N,4)
+    u: torch.Tensor          # (B,T,2)
+    K: torch.Tensor          # (B,T,2,4)  gains of each lane's last iteration
+    sigma: torch.Tensor      # (B,T,2)
+    cost: torch.Tensor       # (B,)
+    n_iter: torch.Tensor     # (B,) outer iterations executed (incl. a final failed one)
+    status: torch.Tensor     # (B,) _lib.CONVERGED / LS_FAILED / MAX_ITERS
+    n_rollouts: torch.Tensor # (B,)
+    gamma: torch.Tensor      # (B,) last accepted step
+    iterations: int          # outer loop iterations run for the whole batch
+    lane_iterations: int     # sum of n_iter over lanes (the throughput numerator)
+    seconds: float           # wall time of the solve loop (init + iterations + finalize)
+    stats_log: list = field(default_factory=list)
+    hist_cost: torch.Tensor | None = None   # (hist_len, B)
+    hist_smax: torch.Tensor | None = None   # (hist_len, B)
+
+
+class BatchedNewtonSolver:
+    """Owns the device buffers of a batch of ``B`` lanes that share x_ref / u_ref."""
+
+    def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
+                 max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0):
+        if B <= 0:
+            raise ValueError("batch must hold at least one lane")
+        self.eng = engine
+        self.x_ref, self.u_ref = engine.refs(x_ref, u_ref)
+        self.B, self.Bp = int(B), padded(int(B))
+        self.N = int(self.x_ref.shape[0])
+        self.T = self.N - 1
+        self.armijo = _lib.GymArmijo(float(tol), float(beta), float(c), float(gamma_0), int(max_ls),
+                                     1 if hist_len > 0 else 0)
+        if max_ls < 1:
+            raise ValueError("max_ls must be >= 1")
+        dev = engine.device
+        e = lambda *s, dt=F64: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
+        Bp, N, T = self.Bp, self.N, self.T
+        self.x = [e(N, 2, Bp, 2), e(N, 2, Bp, 2)]
+        self.u = [e(T, 1, Bp, 2), e(T, 1, Bp, 2)]
+        self.K1 = e(T, 2, Bp, 2)
+        self.sigma = e(T, 1, Bp, 2)
+        self.cost, self.dJ, self.smax, self.gamma = e(Bp), e(Bp), e(Bp), e(Bp)
+        i32 = torch.int32
+        self.status, self.n_iter, self.res_buf, self.n_roll = (e(Bp, dt=i32) for _ in range(4))
+        self.retry_list = e(Bp, dt=i32)
+        self.counters = torch.zeros(4, dtype=i32, device=dev)
+        self.cand_ok = torch.zeros((max(int(max_ls), 1), Bp), dtype=torch.uint8, device=dev)
+        self.partials = e(256 * 8)
+        self.stats = torch.zeros(8, dtype=F64, device=dev)
+        self.hist_len = int(hist_len)
+        self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
+        self.hist_smax = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
+        self.K1.zero_(); self.sigma.zero_()
+        b = _lib.GymBatch()
+        b.B, b.Bp, b.N, b.hist_len = self.B, self.Bp, self.N, self.hist_len
+        b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
+        b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
+        for name in ("K1", "sigma", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
+                     "retry_list", "counters", "cand_ok", "partials", "stats"):
+            setattr(b, name, getattr(self, name).data_ptr())
+        b.x_ref, b.u_ref = self.x_ref.data_ptr(), self.u_ref.data_ptr()
+        b.hist_cost = _lib.ptr(self.hist_cost)
+        b.hist_smax = _lib.ptr(self.hist_smax)
+        self.batch = b
+        self.k = 0
+        self.timing = None
+
+    # --- optional per-kernel HIP-event timing (on the solver's stream) ---------------------
+    def enable_timing(self):
+        if self.timing is None:
+            t = _lib.GymTiming()
+            _lib.check(self.eng.lib.gym_timing_create(C.byref(t)), "gym_timing_create")
+            self.timing = t
+            self.batch.timing = C.pointer(t)
+        return self
+
+    def reset_timing(self):
+        if self.timing is not None:
+            for i in range(5):
+                self.timing.ms[i] = 0.0
+                self.timing.launches[i] = 0
+            self.timing.pending = 0
+
+    def collect_timing(self):
+        """Accumulate recorded event pairs; the stream must have been synchronised."""
+        if self.timing is not None:
+            _lib.check(self.eng.lib.gym_timing_collect(C.byref(self.timing)), "gym_timing_collect")
+
+    def kernel_times(self) -> dict:
+        """{kind: (total_ms, launches)} for kinds _lib.KERNEL_KINDS."""
+        if self.timing is None:
+            return {}
+        return {k: (float(self.timing.ms[i]), int(self.timing.launches[i])) for i, k in enumerate(_lib.KERNEL_KINDS)}
+
+    def __del__(self):
+        t = getattr(self, "timing", None)
+        if t is not None:
+            try:
+                self.eng.lib.gym_timing_destroy(C.byref(t))
+            except Exception:
+                pass
+
+    # --- the three stream-ordered phases (no host synchronisation inside) -----------------
+    def init(self, x0):
+        x0 = self.eng.t(x0).reshape(-1, 4)
+        if x0.shape[0] != self.B:
+            raise ValueError(f"x0 must hold {self.B} lanes, got {x0.shape[0]}")
+        self._x0 = x0
+        _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
+                                                C.byref(self.batch), self.eng.stream), "gym_newton_init")
+        self.k = 0
+
+    def iteration(self) -> torch.Tensor:
+        _lib.check(self.eng.lib.gym_newton_iteration(C.byref(self.eng.model), C.byref(self.eng._w),
+                                                     C.byref(self.armijo), C.byref(self.batch), self.k,
+                                                     self.eng.stream), "gym_newton_iteration")
+        self.k += 1
+        return self.stats
+
+    def finalize(self):
+        B, N, T, dev = self.B, self.N, self.T, self.eng.device
+        x = torch.empty((B, N, 4), dtype=F64, device=dev)
+        u = torch.empty((B, T, 2), dtype=F64, device=dev)
+        K = torch.empty((B, T, 2, 4), dtype=F64, device=dev)
+        s = torch.empty((B, T, 2), dtype=F64, device=dev)
+        _lib.check(self.eng.lib.gym_newton_finalize(C.byref(self.batch), self.k, x.data_ptr(), u.data_ptr(),
+                                                    K.data_ptr(), s.data_ptr(), self.eng.stream),
+                   "gym_newton_finalize")
+        return x, u, K, s
+
+    # --- full solve ----------------------------------------------------------------------
+    def solve(self, x0, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,
+              keep_stats: bool = False) -> SolveResult:
+        """Run until every lane (of every rank, if ``reduce_stats`` all-reduces) is done or max_iters."""
+        torch.cuda.synchronize(self.eng.device)
+        t0 = time.perf_counter()
+        self.init(x0)
+        log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every, log_every=log_every,
+                          keep_stats=keep_stats)
+        x, u, K, s = self.finalize()
+        torch.cuda.synchronize(self.eng.device)
+        secs = time.perf_counter() - t0
+        B = self.B
+        n_iter = self.n_iter[:B].clone()
+        return SolveResult(
+            x=x, u=u, K=K, sigma=s, cost=self.cost[:B].clone(), n_iter=n_iter, status=self.status[:B].clone(),
+            n_rollouts=self.n_roll[:B].clone(), gamma=self.gamma[:B].clone(), iterations=self.k,
+            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log,
+            hist_cost=None if self.hist_cost is None else self.hist_cost[:, :B].clone(),
+            hist_smax=None if self.hist_smax is None else self.hist_smax[:, :B].clone())
+
+
+def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,
+                keep_stats: bool = False) -> list:
+    """Outer Newton loop shared by every stepper (HIP solver; the test oracle stepper).
+
+    ``stepper.iteration()`` enqueues one iteration for all of its lanes and returns the 8-entry
+    statistics tensor (STAT_FIELDS).  Every ``sync_every`` iterations the statistics are
+    all-reduced across ranks (``reduce_stats``, SUM) and read on the host; the loop stops when no
+    lane of any rank is active.  Returns the list of host statistics if ``keep_stats``."""
+    log = []
+    for k in range(int(max_iters)):
+        st = stepper.iteration()
+        if (k + 1) % sync_every == 0 or k + 1 == max_iters:
+            if reduce_stats is not None:
+                st = reduce_stats(st)
+            host = st.cpu().numpy() if isinstance(st, torch.Tensor) else np.asarray(st)
+            collect = getattr(stepper, "collect_timing", None)
+            if collect is not None:
+                collect()
+            if keep_stats:
+                log.append(host.copy())
+            if log_every and (k % log_every == 0):
+                print(f"iter {k}: active={int(host[0])} sumJ={host[1]:.6e} ran={int(host[3])} "
+                      f"retry={int(host[4])}", flush=True)
+            if host[0] == 0:
+                break
+    return log
+
+
+def newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
+                       max_ls=MAX_LINE_SEARCH_ITERS, engine: AcrobotEngine | None = None, hist_len=0,
+                       reduce_stats=None) -> SolveResult:
+    """Batched newton_Algorithm: x0 (B,4) -> SolveResult (device tensors)."""
+    eng = engine or AcrobotEngine()
+    x0 = eng.t(x0).reshape(-1, 4)
+    solver = BatchedNewtonSolver(eng, x_ref, u_ref, x0.shape[0], tol=tol, beta=beta, c=c, gamma_0=gamma_0,
+                                 max_ls=max_ls, hist_len=hist_len)
+    return solver.solve(x0, max_iters, reduce_stats=reduce_stats)

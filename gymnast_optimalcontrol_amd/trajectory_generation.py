@@ -1,0 +1,244 @@
+"""Drop-in for the reference's ``trajectory_generation.py`` hot path, computed by the HIP engine.
+
+Same module constants (T, N, nu, nx, Q, R, Q_T; :8-18), same functions with the reference's
+argument order, defaults, return structure and error behaviour:
+
+  simulate_open_loop (:74)          -> gym_rollout_open_loop
+  derivatives_Cost (:89)            -> gym_stage_cost_derivs
+  stage_blocks_and_affine (:116), terminal_blocks (:131)   (via derivatives_Cost)
+  compute_costate_trajectory (:138) -> gym_backward_sweep (costate output)
+  discretize_linearization (:161)   (4x4 host glue; the same map is fused in the kernels)
+  build_stage_lists (:166)          -> gym_linearize
+  calculate_K_and_sigma (:183)      -> gym_riccati_general
+  forward_closed_loop_update (:218) -> gym_closed_loop
+  total_cost (:231)                 -> gym_total_cost
+  newton_Algorithm (:298)           -> gym_newton_init / gym_newton_iteration / gym_newton_finalize
+  get_fully_actuated_ref (:511), compute_equilibrium (:22), define_reference_piecewise (:41)
+                                    (problem setup on the host, as in the reference)
+
+Like the reference, the weights are read from this module's globals Q, R, Q_T at call time.
+Batched variants (``*_batch``) take stacks of lanes and return device tensors.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dynamics import (Calculate_A_B_matrixes, continuous_dynamics, dt, dynamics, engine, ni, ns,  # noqa: F401
+                       set_params, use_params)
+from .engine import Weights
+from .params import MAX_LINE_SEARCH_ITERS
+from .solver import BatchedNewtonSolver, SolveResult, newton_solve_batch  # noqa: F401
+
+T = 10.0
+N = int(T / dt) + 1
+nu = 2
+nx = 4
+
+Q = np.diag([130.0, 30.0, 0.0001, 0.0001])
+R = np.diag([1e-6, 1.5])
+Q_T = np.diag([130, 130., 1., 1.0])
+
+
+def _eng():
+    e = engine()
+    e.set_weights(Weights.from_matrices(Q, R, Q_T))
+    return e
+
+
+# ------------------------------------------------------------------------------ problem setup
+def compute_equilibrium(u_target, theta_guess):
+    """Solve G(theta1, theta2) = u_target (:22-39) with scipy's hybrid root finder."""
+    from scipy.optimize import root
+    _, _, G, _ = set_params(1)
+    u_target = np.asarray(u_target, dtype=float)
+    sol = root(lambda th: np.asarray(G(th[0], th[1]), dtype=float).reshape(-1) - u_target, theta_guess,
+               method="hybr")
+    if not sol.success:
+        raise RuntimeError("Root finder failed: " + sol.message)
+    return np.array([sol.x[0], sol.x[1], 0.0, 0.0]), np.array(u_target, dtype=float).reshape(-1)
+
+
+def define_reference_piecewise(T, x_e1, x_e2, u_e1, u_e2):
+    """Two constant segments: x_e1 for t < T/2, x_e2 after (:41-58)."""
+    Nn = int(T / dt) + 1
+    t_ref = np.linspace(0.0, T, Nn)
+    first = (t_ref < T / 2.0)[:, None]
+    x_ref = np.where(first, np.asarray(x_e1, float)[None], np.asarray(x_e2, float)[None])
+    u_ref = np.where(first, np.asarray(u_e1, float)[None], np.asarray(u_e2, float)[None])
+    return t_ref, x_ref, u_ref
+
+
+def get_fully_actuated_ref(path="trajectories_npz/fully_actuated_trajectory.npz"):
+    """Task-2 reference (:511-518): x_ref, 2*[0, u_fa[:,1]], time.  ``path`` is CWD-relative as in the reference."""
+    data = np.load(path)
+    u_ref = np.zeros(data["u"].shape)
+    u_ref[:, 1] = data["u"][:, 1]
+    return data["x"], np.multiply(u_ref, 2), data["time"]
+
+
+# ---------------------------------------------------------------------------- stage primitives
+def derivatives_Cost(x, x_ref, u, u_ref, Q, R, Q_T=None, terminal=False):
+    """Stage (l, q, r, 2Q, 2R) or terminal (l_T, q_T, 2Q_T) cost derivatives (:89-114)."""
+    e = engine()
+    if not terminal:
+        l, gx, gu = e.stage_cost_derivs(np.asarray(x, float), np.asarray(x_ref, float), np.asarray(u, float),
+                                        np.asarray(u_ref, float), Q, R, terminal=False)
+        return float(l[0]), gx[0].cpu().numpy(), gu[0].cpu().numpy(), 2 * Q, 2 * R
+    l, gx, _ = e.stage_cost_derivs(np.asarray(x, float), np.asarray(x_ref, float), None, None, Q_T, None,
+                                   terminal=True)
+    return float(l[0]), gx[0].cpu().numpy(), 2 * Q_T
+
+
+def stage_blocks_and_affine(x, u, x_ref, u_ref, Q, R, A, B, lambda_next):
+    """Gauss-Newton stage blocks (Q_t, R_t, S_t = 0, q_t, r_t) (:116-129)."""
+    _, grad_x, grad_u, hess_xx, hess_uu = derivatives_Cost(x, x_ref, u, u_ref, Q, R, terminal=False)
+    return hess_xx, hess_uu, np.zeros((u.shape[0], x.shape[0])), grad_x, grad_u
+
+
+def terminal_blocks(x_T, x_ref_T, Q_T):
+    """(Q_T block, q_T) (:131-136)."""
+    _, grad_xT, hess_xx = derivatives_Cost(x_T, x_ref_T, np.zeros(nu), np.zeros(nu), Q=None, R=None, Q_T=Q_T,
+                                           terminal=True)
+    return hess_xx, grad_xT
+
+
+def discretize_linearization(Ac, Bc, dt):
+    """Forward-Euler A_d = I + dt A_c, B_d = dt B_c (:161-164)."""
+    return np.eye(Ac.shape[0]) + dt * Ac, dt * Bc
+
+
+# ------------------------------------------------------------------------- trajectory functions
+def _zeros_refs(Nn):
+    return np.zeros((Nn, 4)), np.zeros((Nn - 1, 2))
+
+
+def simulate_open_loop(x0, u_traj):
+    """Roll x0 forward under u_traj with RK4 (:74-87) -> (len(u)+1, nx)."""
+    u_traj = np.asarray(u_traj, dtype=float)
+    xr, ur = _zeros_refs(u_traj.shape[0] + 1)
+    x, _ = _eng().rollout_open_loop(np.asarray(x0, float).reshape(1, 4), u_traj[None], xr, ur)
+    return x[0].cpu().numpy()
+
+
+def compute_costate_trajectory(x_traj, u_traj, x_ref, u_ref):
+    """Costates lambda_N = 2 Q_T dx_N, lambda_t = 2 Q dx_t + A_d^T lambda_{t+1} (:138-159) -> list of N (4,)."""
+    Nn = x_traj.shape[0]
+    _, _, _, _, lam = _eng().backward(np.asarray(x_traj, float)[None], np.asarray(u_traj, float)[None][:, :Nn - 1],
+                                      np.asarray(x_ref, float)[:Nn], np.asarray(u_ref, float)[:Nn - 1],
+                                      want_lambda=True)
+    lam = lam[0].cpu().numpy()
+    return [lam[t] for t in range(Nn)]
+
+
+def build_stage_lists(x_traj, u_traj, x_ref, u_ref, lambda_seq):
+    """Per-stage A_d, B_d, Q_t, R_t, S_t, q_t, r_t and the terminal blocks (:166-181)."""
+    Nn = x_traj.shape[0]
+    Ad, Bd, q, r, qT = _eng().linearize(np.asarray(x_traj, float)[None], np.asarray(u_traj, float)[None][:, :Nn - 1],
+                                        np.asarray(x_ref, float)[:Nn], np.asarray(u_ref, float)[:Nn - 1])
+    Ad, Bd, q, r, qT = (a[0].cpu().numpy() for a in (Ad, Bd, q, r, qT))
+    Tn = Nn - 1
+    return ([Ad[t] for t in range(Tn)], [Bd[t] for t in range(Tn)], [2 * Q for _ in range(Tn)],
+            [2 * R for _ in range(Tn)], [np.zeros((nu, nx)) for _ in range(Tn)], [q[t] for t in range(Tn)],
+            [r[t] for t in range(Tn)], 2 * Q_T, qT)
+
+
+def calculate_K_and_sigma(A_list, B_list, Q_list, R_list, S_list, q_list, r_list, Q_T_block, q_T):
+    """Backward Riccati recursion on general stage data (:183-216) -> (K list, sigma list, dJ)."""
+    K, sig, dJ = engine().riccati_general(np.asarray(A_list)[None], np.asarray(B_list)[None], np.asarray(Q_list)[None],
+                                          np.asarray(R_list)[None], np.asarray(S_list)[None], np.asarray(q_list)[None],
+                                          np.asarray(r_list)[None], np.asarray(Q_T_block)[None],
+                                          np.asarray(q_T)[None])
+    K, sig = K[0].cpu().numpy(), sig[0].cpu().numpy()
+    return [K[t] for t in range(K.shape[0])], [sig[t] for t in range(sig.shape[0])], float(dJ[0])
+
+
+def forward_closed_loop_update(x_traj, u_traj, K, sigma, gamma=1.0):
+    """u_new = u + K (x_new - x) + gamma sigma, RK4 rollout (:218-229) -> (x_new, u_new)."""
+    Nn = x_traj.shape[0]
+    xr, ur = _zeros_refs(Nn)
+    xn, un, _ = _eng().closed_loop(np.asarray(x_traj, float)[None], np.asarray(u_traj, float)[None][:, :Nn - 1],
+                                   np.asarray(K, float)[None], np.asarray(sigma, float)[None], float(gamma), xr, ur)
+    u_new = np.asarray(u_traj, dtype=float).copy()
+    u_new[:Nn - 1] = un[0].cpu().numpy()
+    return xn[0].cpu().numpy(), u_new
+
+
+def total_cost(x_traj, u_traj, x_ref, u_ref, Q, R, Q_T):
+    """J = sum_t dx'Q dx + du'R du + dx_N' Q_T dx_N (:231-252)."""
+    Nn = x_traj.shape[0]
+    J = engine().total_cost(np.asarray(x_traj, float)[None], np.asarray(u_traj, float)[None][:, :Nn - 1],
+                            np.asarray(x_ref, float)[:Nn], np.asarray(u_ref, float)[:Nn - 1], Q, R, Q_T)
+    return float(J[0])
+
+
+def plot_armijo_line_search(*args, **kwargs):
+    """Plotting is out of scope of the accelerated path (reference :254-296); intentionally a no-op."""
+    return None
+
+
+# ------------------------------------------------------------------------------ the solver
+def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1, plot_armijo_iters=10,
+                     verbose=True):
+    """Regularised Newton's method for optimal control with Armijo line search (:298-398).
+
+    Returns (x_traj (N,4), u_traj (N-1,2), K (list of (2,4)), sigma (list of (2,)), history) where
+    history has 'cost', 'sigma_norm', 'x_trajs', 'sigmas' exactly as the reference fills them."""
+    x_ref = np.asarray(x_ref, dtype=float)
+    u_ref = np.asarray(u_ref, dtype=float)
+    if u_ref.shape[0] == x_ref.shape[0]:
+        if verbose:
+            print(f" u_ref has same length as x_ref ({u_ref.shape[0]}). Using first N-1 controls.")
+        u_ref = u_ref[:-1]
+    if u_ref.shape[0] != x_ref.shape[0] - 1:
+        raise ValueError(f"Incompatible dimensions: x_ref has {x_ref.shape[0]} states but u_ref has "
+                         f"{u_ref.shape[0]} controls (expected {x_ref.shape[0]-1})")
+    eng = _eng()
+    solver = BatchedNewtonSolver(eng, x_ref, u_ref, 1, tol=tol, beta=beta, c=c, gamma_0=gamma_0,
+                                 max_ls=MAX_LINE_SEARCH_ITERS)
+    x0 = np.asarray(x0, dtype=float).reshape(1, 4)
+    solver.init(x0)
+    Tn = x_ref.shape[0] - 1
+
+    def lane_x(buf):
+        return eng.unpack(solver.x[buf], 1)[0].cpu().numpy()
+
+    def lane_sigma():
+        return eng.unpack(solver.sigma, 1)[0].cpu().numpy()
+
+    x_traj = lane_x(0)
+    assert x_traj.shape[0] == x_ref.shape[0], \
+        f"Simulated trajectory length mismatch: {x_traj.shape[0]} vs {x_ref.shape[0]}"
+    cost_k = float(solver.cost[0].item())
+    history = {"cost": [cost_k], "sigma_norm": [], "x_trajs": [x_traj.copy()], "sigmas": []}
+    for k in range(max_iters):
+        prev_cost = cost_k
+        solver.iteration()
+        status = int(solver.status[0].item())
+        sig = lane_sigma()
+        history["sigmas"].append([sig[t].copy() for t in range(Tn)])
+        history["sigma_norm"].append(float(solver.smax[0].item()))
+        if status == _lib.LS_FAILED:
+            if verbose:
+                print(f"Iteration {k}: Line search failed to find sufficient decrease.")
+            break
+        cost_k = float(solver.cost[0].item())
+        history["cost"].append(cost_k)
+        history["x_trajs"].append(lane_x(solver.k & 1))
+        if verbose and k % 10 == 0:
+            print(f"Iter {k}: Cost={cost_k:.2f}, diff_cost={prev_cost - cost_k:.2e}, ")
+        if status == _lib.CONVERGED:
+            if verbose:
+                print(f"Converged at iteration {k}!")
+            break
+    x, u, K, s = solver.finalize()
+    K = K[0].cpu().numpy(); s = s[0].cpu().numpy()
+    return (x[0].cpu().numpy(), u[0].cpu().numpy(), [K[t] for t in range(Tn)], [s[t] for t in range(Tn)], history)
+
+
+def newton_Algorithm_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
+                           max_ls=MAX_LINE_SEARCH_ITERS, hist_len=0, reduce_stats=None) -> SolveResult:
+    """Batched newton_Algorithm over lanes x0 (B,4) sharing (x_ref, u_ref) -> SolveResult (device tensors)."""
+    return newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=tol, beta=beta, c=c, gamma_0=gamma_0, max_ls=max_ls,
+                              engine=_eng(), hist_len=hist_len, reduce_stats=reduce_stats)

@@ -1,0 +1,195 @@
+/*
+ * gymnast_acrobot.h -- C-ABI of the MI355X (gfx950) batched acrobot Newton/Armijo engine.
+ *
+ * Drop-in boundary for the reference's hot path (francescoolivieri/Gymnast_OptimalControl):
+ * the Python module surface of dynamics.py / trajectory_generation.py is re-implemented by
+ * gymnast_optimalcontrol_amd/{dynamics,trajectory_generation}.py on top of these entry points
+ * (ctypes).  Every entry point cites the reference function it replaces.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless marked [host].
+ *   - `stream` is a hipStream_t passed as void* (0 = null stream).  Work is stream-ordered;
+ *     no entry point synchronises the device (gym_timing_collect only reads events the
+ *     caller has already synchronised).
+ *   - Return value: 0 on success, otherwise a hipError_t code (launch / argument errors:
+ *     GYM_EINVAL).  Per-lane numerical outcomes are reported in status arrays, never as errors.
+ *   - Callers own every buffer; kernels never allocate.
+ *   - fp64 (IEEE binary64) throughout.
+ *
+ * Layouts
+ *   lane-major  : the reference's own arrays stacked over lanes: x (B,N,4), u (B,T,2),
+ *                 K (B,T,2,4), sigma (B,T,2), row-major.
+ *   SoA "pairs" : time-major, lane-innermost, two components per 16-byte element so that a
+ *                 wavefront reads 1 KiB contiguous per load instruction:
+ *                   states  x   : (N, 2, Bp) double2   pairs (th1,th2), (w1,w2)
+ *                   controls u  : (T, Bp)    double2   (tau1, tau2)
+ *                   gains   K1  : (T, 2, Bp) double2   row 1 of K_t (row 0 is identically 0)
+ *                   gains   Kf  : (T, 4, Bp) double2   full K_t, pairs (K00,K01)(K02,K03)(K10,K11)(K12,K13)
+ *                   sigma   s   : (T, Bp)    double2
+ *                 Bp = lane stride (>= B, multiple of 64).
+ */
+#ifndef GYMNAST_ACROBOT_H
+#define GYMNAST_ACROBOT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GYM_ABI_VERSION 1
+#define GYM_EINVAL 1  /* == hipErrorInvalidValue */
+
+/* Lane status codes (per-lane outcome of newton_Algorithm, trajectory_generation.py:329-396). */
+enum {
+    GYM_ACTIVE = 0,     /* still iterating                                              */
+    GYM_CONVERGED = 1,  /* max|sigma| < tol after an accepted step            (:394-396) */
+    GYM_LS_FAILED = 2,  /* Armijo exhausted max_ls trials, no update          (:367-369) */
+    GYM_MAX_ITERS = 3,  /* loop ran out of iterations                          (:329)    */
+    GYM_PAD = 4         /* padding lane (lane >= B)                                     */
+};
+
+/* Acrobot model, reduced to the coefficients the dynamics use (dynamics.py:63-90):
+ *   M11 = a + 2 b cos(th2), M12 = d + b cos(th2), M22 = d,
+ *   C   = b sin(th2) [[-w2, -(w1+w2)], [w1, 0]],   G = [g1 sin th1 + g2 sin(th1+th2), g2 sin(th1+th2)],
+ *   F   = diag(f1, f2);  tau = [0, u1] (dynamics.py:153, :205);  dt = RK4 / Euler step. */
+typedef struct gym_model {
+    double a, b, d, g1, g2, f1, f2, dt;
+} gym_model;
+
+/* Diagonal cost weights (trajectory_generation.py:16-18): stage Q, R; terminal Q_T. */
+typedef struct gym_weights {
+    double Q[4], R[2], QT[4];
+} gym_weights;
+
+/* Armijo / stopping parameters (newton_Algorithm kwargs, trajectory_generation.py:298, :345). */
+typedef struct gym_armijo {
+    double tol, beta, c, gamma0;
+    int32_t max_ls;     /* 20 in the reference (:345) */
+    int32_t record_history;
+} gym_armijo;
+
+/* Optional per-kernel timing of gym_newton_iteration with HIP events on the solver's stream.
+ * Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
+ * rollout, 4 statistics.  A pair is recorded only if the previous one was collected. */
+#define GYM_NK 5
+typedef struct gym_timing {
+    void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
+    double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
+    int64_t launches[GYM_NK];/* collected launches per kernel kind                        */
+    int32_t pending;         /* bitmask: pairs recorded but not yet collected            */
+    int32_t pad;
+} gym_timing;
+
+/* Device state of a batched solve (all device pointers, sizes in lanes / knots). */
+typedef struct gym_batch {
+    int64_t B, Bp;      /* lanes, lane stride (multiple of 64)                     */
+    int32_t N, hist_len;/* knots (T = N-1); rows of the optional history buffers   */
+    double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered   */
+    double* u[2];       /* (T,Bp)   double2 control trajectories                  */
+    double* K1;         /* (T,2,Bp) double2 feedback gains, row 1                 */
+    double* sigma;      /* (T,Bp)   double2 feed-forward                          */
+    const double* x_ref;/* (N,4) shared reference states                          */
+    const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
+    double* cost;       /* (Bp) current J_k                                       */
+    double* dJ;         /* (Bp) expected reduction sum g^T sigma                  */
+    double* smax;       /* (Bp) max|sigma| of the last backward sweep             */
+    double* gamma;      /* (Bp) last accepted step size                           */
+    int32_t* status;    /* (Bp) GYM_* codes                                       */
+    int32_t* n_iter;    /* (Bp) outer iterations executed (incl. a final failed)  */
+    int32_t* res_buf;   /* (Bp) which x/u buffer holds a finished lane's result   */
+    int32_t* n_roll;    /* (Bp) closed-loop rollouts evaluated                     */
+    int32_t* retry_list;/* (Bp) lanes that need Armijo trials 2..max_ls           */
+    int32_t* counters;  /* (4)  [0] = retry count                                 */
+    uint8_t* cand_ok;   /* (max_ls, Bp) Armijo acceptance of candidate j           */
+    double* partials;   /* (256*8) per-block statistics                           */
+    double* stats;      /* (8) see gym_newton_iteration                           */
+    double* hist_cost;  /* optional (hist_len, Bp): J after iteration k            */
+    double* hist_smax;  /* optional (hist_len, Bp): max|sigma| of iteration k      */
+    gym_timing* timing; /* [host] optional kernel timing (NULL: none)               */
+} gym_batch;
+
+int gym_abi_version(void);
+
+/* [host] Reduce a reference parameter set {m1,m2,l1,lc1,l2,lc2,I1,I2,g,f1,f2} (dynamics.py:15-61). */
+int gym_model_from_params(const double params[11], double dt, gym_model* out);
+
+/* ---------------- per-point primitives (lane-major x (n,4), u (n,2)) ---------------- */
+/* dynamics.py:197-213 continuous_dynamics -> xdot (n,4) */
+int gym_continuous_dynamics(const gym_model* m, const double* x, const double* u, double* xdot, int64_t n, void* stream);
+/* dynamics.py:177-195 dynamics (RK4 step) -> xnext (n,4) */
+int gym_rk4_step(const gym_model* m, const double* x, const double* u, double* xnext, int64_t n, void* stream);
+/* dynamics.py:217-226 Calculate_A_B_matrixes -> A_c (n,4,4), B_c (n,4,2) */
+int gym_jacobians(const gym_model* m, const double* x, const double* u, double* A_c, double* B_c, int64_t n, void* stream);
+/* trajectory_generation.py:89-114 derivatives_Cost (general Q (4,4), R (2,2) or Q_T) [host matrices]:
+ * terminal == 0: l (n), gx (n,4), gu (n,2);  terminal != 0: l (n), gx (n,4) with Q_T, gu unused. */
+int gym_stage_cost_derivs(const double* x, const double* xr, const double* u, const double* ur, const double Q[16],
+                          const double R[4], int32_t terminal, double* l, double* gx, double* gu, int64_t n, void* stream);
+
+/* ---------------- layout transposes ---------------- */
+/* lane-major (B,L,C) -> SoA (L,C/2,Bp) double2; C even.  Padding lanes are zero-filled. */
+int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, void* stream);
+/* SoA -> lane-major; if sel != NULL lane b reads from (sel[b] ? src1 : src0). */
+int gym_unpack_lanes(const double* src0, const double* src1, const int32_t* sel, double* dst, int64_t B, int64_t Bp,
+                     int32_t L, int32_t C, void* stream);
+/* compact gains K1 (T,2,Bp) -> full lane-major K (B,T,2,4) with row 0 = 0 */
+int gym_unpack_gains(const double* K1, double* K, int64_t B, int64_t Bp, int32_t T, void* stream);
+
+/* ---------------- trajectory kernels (SoA) ---------------- */
+/* trajectory_generation.py:74-87 simulate_open_loop: x0 (B,4) lane-major, u (T,Bp) SoA -> x (N,2,Bp);
+ * if cost != NULL also total_cost (:231-252) of (x,u) with diagonal weights. */
+int gym_rollout_open_loop(const gym_model* m, const gym_weights* w, const double* x0, const double* u,
+                          const double* x_ref, const double* u_ref, double* x, double* cost, int64_t B, int64_t Bp,
+                          int32_t N, void* stream);
+/* trajectory_generation.py:218-229 forward_closed_loop_update with FULL gains Kf (T,4,Bp) and per-lane gamma (Bp);
+ * writes x_new (N,2,Bp), u_new (T,Bp); cost (Bp) of the new trajectory if non-NULL. */
+int gym_closed_loop(const gym_model* m, const gym_weights* w, const double* x, const double* u, const double* Kf,
+                    const double* sigma, const double* gamma, const double* x_ref, const double* u_ref,
+                    double* x_new, double* u_new, double* cost, int64_t B, int64_t Bp, int32_t N, void* stream);
+/* trajectory_generation.py:231-252 total_cost with general Q, R, Q_T [host matrices]. */
+int gym_total_cost(const double* x, const double* u, const double* x_ref, const double* u_ref, const double Q[16],
+                   const double R[4], const double QT[16], double* cost, int64_t B, int64_t Bp, int32_t N, void* stream);
+/* Fused backward sweep = compute_costate_trajectory (:138-159) + build_stage_lists (:166-181) +
+ * calculate_K_and_sigma (:183-216) for the Gauss-Newton blocks (2Q, 2R, S = 0, terminal 2Q_T):
+ * K1 (T,2,Bp), sigma (T,Bp), dJ (Bp), smax = max|sigma| (Bp); lambda (N,2,Bp) costates if non-NULL. */
+int gym_backward_sweep(const gym_model* m, const gym_weights* w, const double* x, const double* u,
+                       const double* x_ref, const double* u_ref, double* K1, double* sigma, double* dJ, double* smax,
+                       double* lambda, int64_t B, int64_t Bp, int32_t N, void* stream);
+/* build_stage_lists (:166-181): A_d (T,16,Bp), B_d (T,8,Bp), q (T,4,Bp), r (T,2,Bp), qT (4,Bp); plain doubles. */
+int gym_linearize(const gym_model* m, const gym_weights* w, const double* x, const double* u, const double* x_ref,
+                  const double* u_ref, double* A_d, double* B_d, double* q, double* r, double* qT, int64_t B,
+                  int64_t Bp, int32_t N, void* stream);
+/* calculate_K_and_sigma (:183-216) on general dense stage data, plain-double SoA:
+ * A (T,16,Bp) B (T,8,Bp) Q (T,16,Bp) R (T,4,Bp) S (T,8,Bp) q (T,4,Bp) r (T,2,Bp) QT (16,Bp) qT (4,Bp)
+ * -> K (T,8,Bp), sigma (T,2,Bp), dJ (Bp).  2x2 solves by LU with partial pivoting (LAPACK dgesv order). */
+int gym_riccati_general(const double* A, const double* Bm, const double* Q, const double* R, const double* S,
+                        const double* q, const double* r, const double* QT, const double* qT, double* K, double* sigma,
+                        double* dJ, int64_t B, int64_t Bp, int32_t T, void* stream);
+
+/* ---------------- batched Newton / Armijo solver (newton_Algorithm, :298-398) ---------------- */
+/* Open-loop init (u = 0, :311-312), J_0 (:319), status/counters reset.  x0 (B,4) lane-major. */
+int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, const gym_batch* bt, void* stream);
+/* One outer iteration k for every ACTIVE lane: backward sweep, Armijo trial 1 (gamma0) fused with its cost,
+ * parallel candidate rollouts gamma0*beta^j (j = 1..max_ls-1) for lanes that rejected trial 1, accepted-
+ * candidate rollout, lane status update, then device statistics into bt->stats:
+ *   [0] lanes still active  [1] sum J over lanes  [2] sum max|sigma|^2 over lanes that ran
+ *   [3] lanes that ran (lane-iterations)  [4] lanes that needed trials >= 2  [5] converged  [6] failed
+ *   [7] rollouts evaluated in total.
+ * Buffer roles: x/u[k&1] = current, x/u[(k+1)&1] = candidate.  Stream-ordered, no host sync. */
+int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt,
+                         int32_t k, void* stream);
+/* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
+ * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) (last iteration's gains), sigma_out (B,T,2). Any output may be NULL. */
+int gym_newton_finalize(const gym_batch* bt, int32_t k_done, double* x_out, double* u_out, double* K_out,
+                        double* sigma_out, void* stream);
+
+/* [host] create / destroy the events of a gym_timing; collect = add the elapsed time of every pending
+ * pair (call only after the stream that recorded them has been synchronised). */
+int gym_timing_create(gym_timing* t);
+int gym_timing_destroy(gym_timing* t);
+int gym_timing_collect(gym_timing* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GYMNAST_ACROBOT_H */

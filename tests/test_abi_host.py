@@ -1,0 +1,170 @@
+"""C-ABI library and host-side logic (CPU only: no kernel is launched here)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gymnast_acrobot.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^int\s+(gym_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_builds_and_exports_every_declared_symbol():
+    from gymnast_optimalcontrol_amd import _build
+    path = _build.build()
+    from gymnast_optimalcontrol_amd import _lib
+    lib = _lib.load(path)
+    declared = _declared()
+    assert declared and set(declared) == set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.gym_abi_version() == 1
+    out = subprocess_nm(path)
+    for name in declared:
+        assert name in out, f"{name} not exported by {path}"
+
+
+def subprocess_nm(path):
+    import subprocess
+    return subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+
+
+def test_library_is_gfx950_code_object(tmp_path):
+    import subprocess
+    from gymnast_optimalcontrol_amd import _build
+    path = _build.build()
+    fb = tmp_path / "fatbin.bin"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, str(fb)], check=True)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o", f"--input={fb}"],
+                         capture_output=True, text=True, check=True)
+    targets = out.stdout.split()
+    assert "hipv4-amdgcn-amd-amdhsa--gfx950" in targets, out.stdout + out.stderr
+
+
+def test_model_from_params_host_call():
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.params import PARAM_SETS, PARAM_NAMES
+    lib = _lib.load()
+    for v, p in PARAM_SETS.items():
+        vec = np.array([p[k] for k in PARAM_NAMES])
+        m = _lib.GymModel()
+        assert lib.gym_model_from_params(vec.ctypes.data, 0.02, C.byref(m)) == 0
+        # M11 = a + 2b cos th2 etc. (dynamics.py:64-67)
+        a = p["I1"] + p["I2"] + p["lc1"] ** 2 * p["m1"] + p["m2"] * (p["l1"] ** 2 + p["lc2"] ** 2)
+        assert m.a == pytest.approx(a) and m.b == pytest.approx(p["m2"] * p["l1"] * p["lc2"])
+        assert m.d == pytest.approx(p["I2"] + p["lc2"] ** 2 * p["m2"])
+        assert m.g1 == pytest.approx(p["g"] * (p["lc1"] * p["m1"] + p["m2"] * p["l1"]))
+        assert m.g2 == pytest.approx(p["g"] * p["m2"] * p["lc2"]) and m.dt == 0.02
+    assert lib.gym_model_from_params(None, 0.02, None) == 1   # GYM_EINVAL, no crash
+
+
+def test_launchers_reject_bad_arguments_without_a_device():
+    """Argument validation happens on the host before any launch."""
+    from gymnast_optimalcontrol_amd import _lib
+    lib = _lib.load()
+    assert lib.gym_pack_lanes(None, None, 4, 64, 3, 4, None) == 1
+    assert lib.gym_pack_lanes(1, 1, 4, 60, 3, 4, None) == 1        # Bp not a multiple of 64
+    assert lib.gym_pack_lanes(1, 1, 4, 64, 3, 3, None) == 1        # odd component count
+    assert lib.gym_newton_iteration(None, None, None, None, 0, None) == 1
+    b = _lib.GymBatch()
+    assert lib.gym_newton_init(None, None, None, C.byref(b), None) == 1
+
+
+def test_shard_range_partitions_exactly():
+    from gymnast_optimalcontrol_amd.distributed import shard_range
+    for total in (1, 7, 64, 1000, 1048576):
+        for world in (1, 2, 3, 8):
+            parts = [shard_range(total, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in parts]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def test_weights_from_matrices():
+    from gymnast_optimalcontrol_amd.engine import Weights, padded
+    w = Weights.from_matrices(np.diag([130.0, 30.0, 1e-4, 1e-4]), np.diag([1e-6, 1.5]), np.diag([130, 130., 1, 1]))
+    assert w.Q == (130.0, 30.0, 1e-4, 1e-4) and w.R == (1e-6, 1.5)
+    with pytest.raises(NotImplementedError):
+        Weights.from_matrices(np.ones((4, 4)), np.eye(2), np.eye(4))
+    with pytest.raises(ValueError):
+        Weights.from_matrices(np.eye(3), np.eye(2), np.eye(4))
+    assert [padded(b) for b in (1, 64, 65, 4096)] == [64, 64, 128, 4096]
+
+
+def test_product_fails_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible")
+    from gymnast_optimalcontrol_amd import dynamics
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        AcrobotEngine()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        dynamics.dynamics(np.zeros(4), np.zeros(2))
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "gymnast_optimalcontrol_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle\b|\boracle/", src, flags=re.M), f
+
+
+def test_reference_surface_names_exist():
+    """The mirror modules expose the reference's names (dynamics.py, trajectory_generation.py)."""
+    from gymnast_optimalcontrol_amd import dynamics as d
+    from gymnast_optimalcontrol_amd import trajectory_generation as tg
+    for n in ("dt", "ns", "ni", "dynamics", "continuous_dynamics", "Calculate_A_B_matrixes", "set_params",
+              "params_1", "params_2", "params_3"):
+        assert hasattr(d, n), n
+    for n in ("T", "N", "nu", "nx", "Q", "R", "Q_T", "compute_equilibrium", "define_reference_piecewise",
+              "simulate_open_loop", "derivatives_Cost", "stage_blocks_and_affine", "terminal_blocks",
+              "compute_costate_trajectory", "discretize_linearization", "build_stage_lists",
+              "calculate_K_and_sigma", "forward_closed_loop_update", "total_cost", "plot_armijo_line_search",
+              "newton_Algorithm", "get_fully_actuated_ref"):
+        assert hasattr(tg, n), n
+    assert tg.N == 501 and d.dt == 0.02 and tg.nx == 4 and tg.nu == 2
+
+
+def test_host_setup_functions_match_reference(golden):
+    """compute_equilibrium / define_reference_piecewise (host-side problem setup) vs the task-1 golden."""
+    from gymnast_optimalcontrol_amd import trajectory_generation as tg
+    g = golden("task1_solve")
+    x_e1, u_e1 = tg.compute_equilibrium(np.array([0.0, 0.0]), (0.1, -0.1))
+    x_e2, u_e2 = tg.compute_equilibrium(np.array([0.5, 0.5]), (0.35, -0.35))
+    np.testing.assert_allclose(x_e1, g["x_e1"], atol=1e-10)
+    np.testing.assert_allclose(x_e2, g["x_e2"], atol=1e-10)
+    t_ref, x_ref, u_ref = tg.define_reference_piecewise(10.0, x_e1, x_e2, u_e1, u_e2)
+    np.testing.assert_allclose(x_ref, g["x_ref"], atol=1e-10)
+    np.testing.assert_allclose(u_ref, g["u_ref_full"], atol=0)
+    np.testing.assert_array_equal(t_ref, g["t_ref"])
+
+
+def test_get_fully_actuated_ref(tmp_path, golden):
+    import shutil
+    from gymnast_optimalcontrol_amd import trajectory_generation as tg
+    os.makedirs(tmp_path / "trajectories_npz")
+    shutil.copy(os.path.join(ROOT, "tests", "golden", "task2_input_fully_actuated.npz"),
+                tmp_path / "trajectories_npz" / "fully_actuated_trajectory.npz")
+    cwd = os.getcwd()
+    try:
+        os.chdir(tmp_path)
+        x_ref, u_ref, t = tg.get_fully_actuated_ref()
+    finally:
+        os.chdir(cwd)
+    g = golden("task2_solve")
+    np.testing.assert_array_equal(x_ref, g["x_ref"])
+    np.testing.assert_array_equal(u_ref, g["u_ref"])
+    np.testing.assert_array_equal(t, g["t_ref"])

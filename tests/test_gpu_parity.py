@@ -1,0 +1,293 @@
+"""Parity of the HIP path (through the C-ABI) against the reference's golden vectors and the oracle.
+
+Tolerances: the kernels use closed-form dynamics/Jacobians and a structure-exploiting Riccati,
+i.e. the reference's arithmetic reordered, so per-primitive results agree to ~1e-12 relative and
+converged trajectories to ~1e-13; the north-star bar for converged trajectories is 1e-8 rel-L2.
+Discrete decisions (iteration counts, Armijo trials, statuses) must match exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+TOL_TRAJ = 1e-8        # north star: converged trajectory within 1e-8 relative L2
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    return AcrobotEngine()
+
+
+@pytest.fixture(scope="module")
+def tg():
+    from gymnast_optimalcontrol_amd import trajectory_generation
+    return trajectory_generation
+
+
+def test_native_library_is_loaded(eng):
+    import ctypes
+    from gymnast_optimalcontrol_amd import _lib
+    assert eng.lib._name == _lib.LIB_PATH
+    assert ctypes.CDLL(_lib.LIB_PATH).gym_abi_version() == 1
+
+
+# ------------------------------------------------------------------------------ primitives
+def test_point_primitives_vs_reference(eng, golden):
+    g = golden("kat_primitives")
+    X, U = g["X"], g["U"]
+    np.testing.assert_allclose(eng.continuous_dynamics(X, U).cpu().numpy(), g["f_cont"], rtol=1e-11, atol=1e-9)
+    np.testing.assert_allclose(eng.rk4(X, U).cpu().numpy(), g["f_rk4"], rtol=1e-11, atol=1e-9)
+    A, B = eng.jacobians(X, U)
+    np.testing.assert_allclose(A.cpu().numpy(), g["A_c"], rtol=1e-10, atol=1e-8)
+    np.testing.assert_allclose(B.cpu().numpy(), g["B_c"], rtol=1e-10, atol=1e-12)
+
+
+def test_reference_style_point_calls(tg, golden):
+    from gymnast_optimalcontrol_amd import dynamics as dyn
+    g = golden("kat_primitives")
+    for i in (0, 1, 2, 3, 4, 5, 17):
+        np.testing.assert_allclose(dyn.dynamics(g["X"][i], g["U"][i]), g["f_rk4"][i], rtol=1e-11, atol=1e-9)
+        np.testing.assert_allclose(dyn.continuous_dynamics(g["X"][i], g["U"][i]), g["f_cont"][i], rtol=1e-11,
+                                   atol=1e-9)
+        A, B = dyn.Calculate_A_B_matrixes(g["X"][i], g["U"][i])
+        assert A.shape == (4, 4) and B.shape == (4, 2)
+        np.testing.assert_allclose(A, g["A_c"][i], rtol=1e-10, atol=1e-8)
+        Ad, Bd = tg.discretize_linearization(A, B, dyn.dt)
+        np.testing.assert_allclose(Ad, g["A_d"][i], rtol=1e-10, atol=1e-10)
+    # column-vector inputs are squeezed like the reference (dynamics.py:181-182)
+    np.testing.assert_allclose(dyn.dynamics(g["X"][0][:, None], g["U"][0][:, None]), g["f_rk4"][0], rtol=1e-11)
+
+
+def test_stage_cost_derivatives(tg, golden):
+    g = golden("kat_primitives")
+    for i in range(0, 64, 9):
+        l, gx, gu, Hx, Hu = tg.derivatives_Cost(g["X"][i], g["xr"][i], g["U"][i], g["ur"][i], g["Qg"], g["Rg"])
+        assert l == pytest.approx(float(g["l"][i]), rel=1e-12)
+        np.testing.assert_allclose(gx, g["gx"][i], rtol=1e-12)
+        np.testing.assert_allclose(gu, g["gu"][i], rtol=1e-12)
+        np.testing.assert_array_equal(Hx, 2 * g["Qg"])
+        lT, gT, HT = tg.derivatives_Cost(g["X"][i], g["xr"][i], g["U"][i], g["ur"][i], None, None, Q_T=g["QTg"],
+                                         terminal=True)
+        assert lT == pytest.approx(float(g["lT"][i]), rel=1e-12)
+        np.testing.assert_allclose(gT, g["gT"][i], rtol=1e-12)
+
+
+# ---------------------------------------------------------------------- one Newton iteration
+@pytest.mark.parametrize("tag", ["it0", "mid"])
+def test_newton_iteration_pieces(tg, golden, tag):
+    g = golden("newton_iteration")
+    x, u, xr, ur = g[f"{tag}_x"], g[f"{tag}_u"], g["x_ref"], g["u_ref"]
+    lam = np.asarray(tg.compute_costate_trajectory(x, u, xr, ur))
+    assert rel_l2(lam, g[f"{tag}_lambda"]) < 1e-12
+    lists = tg.build_stage_lists(x, u, xr, ur, list(lam))
+    np.testing.assert_allclose(np.asarray(lists[0]), g[f"{tag}_A_d"], rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(np.asarray(lists[1]), g[f"{tag}_B_d"], rtol=1e-11, atol=1e-14)
+    np.testing.assert_allclose(np.asarray(lists[5]), g[f"{tag}_q"], rtol=1e-13)
+    np.testing.assert_allclose(np.asarray(lists[6]), g[f"{tag}_r"], rtol=1e-13)
+    np.testing.assert_allclose(lists[8], g[f"{tag}_qT"], rtol=1e-13)
+    K, sig, dJ = tg.calculate_K_and_sigma(*lists)          # generic dense Riccati kernel
+    assert rel_l2(np.asarray(K), g[f"{tag}_K"]) < 1e-10
+    assert rel_l2(np.asarray(sig), g[f"{tag}_sigma"]) < 1e-10
+    assert dJ == pytest.approx(float(g[f"{tag}_dJ"]), rel=1e-10)
+    for gam, sfx in ((0.1, "01"), (1.0, "1")):
+        xn, un = tg.forward_closed_loop_update(x, u, g[f"{tag}_K"], g[f"{tag}_sigma"], gamma=gam)
+        assert rel_l2(xn, g[f"{tag}_xn{sfx}"]) < 1e-10
+        assert rel_l2(un, g[f"{tag}_un{sfx}"]) < 1e-10
+        J = tg.total_cost(xn, un, xr, ur, tg.Q, tg.R, tg.Q_T)
+        assert J == pytest.approx(float(g[f"{tag}_cost{sfx}"]), rel=1e-11)
+    assert tg.total_cost(x, u, xr, ur, tg.Q, tg.R, tg.Q_T) == pytest.approx(float(g[f"{tag}_cost"]), rel=1e-13)
+
+
+@pytest.mark.parametrize("tag", ["it0", "mid"])
+def test_fused_backward_sweep(eng, golden, tag):
+    """The solver's fused structured sweep equals the reference's dense K, sigma, dJ, max|sigma|."""
+    g = golden("newton_iteration")
+    K, sig, dJ, smax, lam = eng.backward(g[f"{tag}_x"][None], g[f"{tag}_u"][None], g["x_ref"], g["u_ref"],
+                                         want_lambda=True)
+    assert rel_l2(K[0].cpu().numpy(), g[f"{tag}_K"]) < 1e-10
+    assert rel_l2(sig[0].cpu().numpy(), g[f"{tag}_sigma"]) < 1e-10
+    assert float(dJ[0]) == pytest.approx(float(g[f"{tag}_dJ"]), rel=1e-10)
+    assert float(smax[0]) == pytest.approx(np.abs(g[f"{tag}_sigma"]).max(), rel=1e-10)
+    assert rel_l2(lam[0].cpu().numpy(), g[f"{tag}_lambda"]) < 1e-12
+    assert np.all(K[0, :, 0, :].cpu().numpy() == 0)
+
+
+def test_general_riccati(tg, golden):
+    g = golden("newton_iteration")
+    K, sig, dJ = tg.calculate_K_and_sigma(list(g["gen_A"]), list(g["gen_B"]), list(g["gen_Q"]), list(g["gen_R"]),
+                                          list(g["gen_S"]), list(g["gen_q"]), list(g["gen_r"]), g["gen_QT"],
+                                          g["gen_qT"])
+    assert rel_l2(np.asarray(K), g["gen_K"]) < 1e-12
+    assert rel_l2(np.asarray(sig), g["gen_sigma"]) < 1e-12
+    assert dJ == pytest.approx(float(g["gen_dJ"]), rel=1e-12)
+
+
+def test_simulate_open_loop(tg, golden):
+    g = golden("newton_iteration")
+    assert rel_l2(tg.simulate_open_loop(g["sim_x0"], g["sim_u"]), g["sim_x"]) < 1e-12
+
+
+# ----------------------------------------------------------------------------- full solves
+def test_task2_newton_algorithm_matches_reference_golden(tg, golden, task2_refs):
+    """main.task_2's call (main.py:65-71) through the drop-in API reproduces acrobot_optimal_trajectory.npz."""
+    xr, ur, _ = task2_refs
+    ref = golden("task2_reference_output")
+    run = golden("task2_solve")
+    x, u, K, sigma, hist = tg.newton_Algorithm(np.array([0, 0, 0, 0]), xr, ur, max_iters=5000, tol=1e-4,
+                                               gamma_0=0.1, plot_armijo_iters=7, verbose=False)
+    assert x.shape == (501, 4) and u.shape == (500, 2) and len(K) == 500 and K[0].shape == (2, 4)
+    assert rel_l2(x, ref["x"]) < TOL_TRAJ
+    assert rel_l2(u, ref["u"]) < TOL_TRAJ
+    assert len(hist["sigma_norm"]) == 393 and len(hist["cost"]) == 394 and len(hist["x_trajs"]) == 394
+    np.testing.assert_allclose(hist["cost"], run["cost_hist"], rtol=1e-9)
+    np.testing.assert_allclose(hist["sigma_norm"], run["sigma_norm_hist"], rtol=1e-6)
+    assert rel_l2(np.asarray(K), run["K"]) < 1e-8
+    assert rel_l2(np.asarray(sigma), run["sigma"]) < 1e-6
+    assert rel_l2(np.asarray(hist["sigmas"][0]), run["sigma_first"]) < 1e-10
+    for j, i in enumerate(run["x_hist_idx"]):
+        assert rel_l2(hist["x_trajs"][i], run["x_hist"][j]) < 1e-9
+
+
+def test_task1_with_live_tau1_channel(tg, golden):
+    g = golden("task1_solve")
+    x, u, K, sigma, hist = tg.newton_Algorithm(g["x0"], g["x_ref"], g["u_ref_full"], max_iters=5000, tol=1e-4,
+                                               gamma_0=0.05, verbose=False)
+    assert len(hist["sigma_norm"]) == int(g["n_iter"]) == 173
+    assert rel_l2(x, g["x"]) < TOL_TRAJ and rel_l2(u, g["u"]) < TOL_TRAJ
+    np.testing.assert_allclose(hist["cost"], g["cost_hist"], rtol=1e-9)
+
+
+def test_batched_lanes_match_reference_decisions(golden, task2_refs):
+    """12 reference lanes incl. backtracking and LS-failure lanes: identical iteration counts, statuses,
+    cost / sigma-norm histories, and trajectories within 1e-8."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    L = golden("lanes")
+    xr, ur, _ = task2_refs
+    B = len(L["names"])
+    s = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1, hist_len=900)
+    r = s.solve(L["x0"], 5000)
+    codes = {1: _lib.CONVERGED, 2: _lib.LS_FAILED}
+    n_iter = r.n_iter.cpu().numpy(); status = r.status.cpu().numpy()
+    hc = r.hist_cost.cpu().numpy(); hs = r.hist_smax.cpu().numpy()
+    for i, name in enumerate(L["names"]):
+        n = int(L["n_iter"][i])
+        assert n_iter[i] == n, name
+        assert status[i] == codes[int(L["status"][i])], name
+        np.testing.assert_allclose(hs[:n, i], L["sigma_norm_hist"][i, :n], rtol=1e-6, err_msg=name)
+        ncost = n if status[i] == _lib.CONVERGED else n - 1
+        np.testing.assert_allclose(hc[:ncost, i], L["cost_hist"][i, 1:ncost + 1], rtol=1e-9, err_msg=name)
+        assert rel_l2(r.x[i].cpu().numpy(), L["x"][i]) < TOL_TRAJ, name
+        assert rel_l2(r.u[i].cpu().numpy(), L["u"][i]) < TOL_TRAJ, name
+        assert rel_l2(r.K[i].cpu().numpy(), L["K"][i]) < 1e-6, name
+    assert r.lane_iterations == int(L["n_iter"].sum())
+
+
+def test_lane_independence_large_batch(golden, task2_refs):
+    """Golden lanes embedded in a 65,536-lane batch give the same results; random lanes agree with the
+    C oracle on decisions and to 1e-8 on trajectories."""
+    from oracle import c_oracle
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    L = golden("lanes")
+    xr, ur, _ = task2_refs
+    B = 65536
+    rng = np.random.default_rng(0)
+    x0 = np.zeros((B, 4))
+    x0[:, :2] = rng.uniform(-0.5, 0.5, (B, 2))
+    idx = np.array([0, 777, 4095, 4096, 30001, 65535, 12, 13, 40000, 40001, 40002, 9])
+    x0[idx] = L["x0"]
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1).solve(x0, 5000)
+    n_iter = r.n_iter.cpu().numpy()
+    for j, i in enumerate(idx):
+        assert n_iter[i] == L["n_iter"][j]
+        assert rel_l2(r.x[i].cpu().numpy(), L["x"][j]) < TOL_TRAJ
+    sample = rng.choice(np.setdiff1d(np.arange(B), idx), 48, replace=False)
+    o = c_oracle.newton_solve(x0[sample], xr, ur, max_iters=5000, tol=1e-4, gamma_0=0.1)
+    np.testing.assert_array_equal(n_iter[sample], o["n_iter"])
+    np.testing.assert_array_equal(r.status.cpu().numpy()[sample], o["status"])
+    for j, i in enumerate(sample):
+        assert rel_l2(r.x[i].cpu().numpy(), o["x"][j]) < TOL_TRAJ
+        assert rel_l2(r.u[i].cpu().numpy(), o["u"][j]) < TOL_TRAJ
+
+
+def test_determinism_bitwise(task2_refs):
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    x0 = np.zeros((300, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (300, 2))
+    s = BatchedNewtonSolver(AcrobotEngine(), xr, ur, 300, tol=1e-4, gamma_0=0.1)
+    a = s.solve(x0, 60, keep_stats=True)
+    b = s.solve(x0, 60, keep_stats=True)
+    assert np.array_equal(a.x.cpu().numpy(), b.x.cpu().numpy())
+    assert np.array_equal(a.cost.cpu().numpy(), b.cost.cpu().numpy())
+    assert np.array_equal(np.asarray(a.stats_log), np.asarray(b.stats_log))
+
+
+@pytest.mark.parametrize("B", [1, 63, 64, 65, 200])
+def test_ragged_batches_and_padding(B, task2_refs):
+    """Lane counts that are not multiples of the wavefront: padding lanes never leak into results/stats."""
+    from oracle import c_oracle
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(B).uniform(-0.5, 0.5, (B, 2))
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1).solve(x0, 25, keep_stats=True)
+    o = c_oracle.newton_solve(x0, xr, ur, max_iters=25, tol=1e-4, gamma_0=0.1)
+    np.testing.assert_array_equal(r.n_iter.cpu().numpy(), o["n_iter"])
+    np.testing.assert_array_equal(r.status.cpu().numpy(), o["status"])     # all MAX_ITERS after 25
+    assert rel_l2(r.x.cpu().numpy(), o["x"]) < 1e-10
+    np.testing.assert_allclose(r.cost.cpu().numpy(), o["cost"], rtol=1e-11)
+    last = r.stats_log[-1]
+    assert last[3] == B and last[0] == B                       # lanes that ran / still active (pre-finalize)
+    assert last[1] == pytest.approx(o["cost"].sum(), rel=1e-10)
+
+
+def test_single_trial_line_search_and_nan_lane(task2_refs):
+    """max_ls = 1 (no retry path) and a NaN initial state (NaN costs compare false -> LS failure)."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from oracle import c_oracle
+    xr, ur, _ = task2_refs
+    x0 = np.zeros((4, 4)); x0[1, :2] = [1.2, -1.0]; x0[2] = np.nan; x0[3, :2] = [-1.4, 1.4]
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, 4, tol=1e-4, gamma_0=1.0, max_ls=1).solve(x0, 200)
+    o = c_oracle.newton_solve(x0, xr, ur, max_iters=200, tol=1e-4, gamma_0=1.0, max_ls=1)
+    np.testing.assert_array_equal(r.n_iter.cpu().numpy(), o["n_iter"])
+    np.testing.assert_array_equal(r.status.cpu().numpy(), o["status"])
+    assert int(r.status[2]) == _lib.LS_FAILED and int(r.n_iter[2]) == 1
+    ok = np.isfinite(o["cost"])
+    assert rel_l2(r.x.cpu().numpy()[ok], o["x"][ok]) < 1e-9
+
+
+def test_u_ref_trim_and_errors(tg, task2_refs):
+    xr, ur, _ = task2_refs
+    ur_full = np.vstack([ur, ur[-1:]])               # N rows -> trimmed (:301-303)
+    x1, u1, *_ = tg.newton_Algorithm(np.zeros(4), xr, ur_full, max_iters=3, tol=1e-4, gamma_0=0.1, verbose=False)
+    x2, u2, *_ = tg.newton_Algorithm(np.zeros(4), xr, ur, max_iters=3, tol=1e-4, gamma_0=0.1, verbose=False)
+    assert np.array_equal(x1, x2) and np.array_equal(u1, u2)
+    with pytest.raises(ValueError, match="Incompatible dimensions"):
+        tg.newton_Algorithm(np.zeros(4), xr, ur[:-3], max_iters=3)
+
+
+def test_full_size_properties(task2_refs):
+    """BASELINE cfg 3 size (262,144 lanes): the golden lane 0 within 1e-8, every headline lane converges
+    in the reference's iteration band, stats are consistent."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    B = 262144
+    x0 = np.zeros((B, 4)); x0[1:, :2] = np.random.default_rng(0).uniform(-0.5, 0.5, (B - 1, 2))
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1).solve(x0, 5000, keep_stats=True)
+    from conftest import load_golden
+    ref = load_golden("task2_reference_output")
+    assert rel_l2(r.x[0].cpu().numpy(), ref["x"]) < TOL_TRAJ
+    st = r.status.cpu().numpy(); n = r.n_iter.cpu().numpy()
+    assert (st == _lib.CONVERGED).all()
+    assert 370 <= n.min() and n.max() <= 420
+    assert r.lane_iterations == int(n.sum()) == int(sum(s[3] for s in r.stats_log))

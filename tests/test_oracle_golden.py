@@ -1,0 +1,132 @@
+"""Pin the CPU oracles (oracle/) to the reference's golden vectors (CPU only).
+
+Golden sources:
+  * task2_reference_output.npz -- the reference's own committed output (main.task_2);
+  * the other fixtures -- produced by running the reference itself (tests/golden/make_golden.py).
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+from oracle import acrobot_np as onp
+from oracle import c_oracle as oc
+
+
+# ----------------------------------------------------------------------------- primitives
+def test_numpy_oracle_primitives_match_reference(golden):
+    g = golden("kat_primitives")
+    X, U = g["X"], g["U"]
+    np.testing.assert_allclose(onp.continuous_dynamics(X, U), g["f_cont"], rtol=1e-11, atol=1e-9)
+    np.testing.assert_allclose(onp.rk4(X, U), g["f_rk4"], rtol=1e-11, atol=1e-9)
+    A, B = onp.jacobians(X, U)
+    np.testing.assert_allclose(A, g["A_c"], rtol=1e-10, atol=1e-8)
+    np.testing.assert_allclose(B, g["B_c"], rtol=1e-10, atol=1e-12)
+    Ad, Bd = onp.discretize(A, B)
+    np.testing.assert_allclose(Ad, g["A_d"], rtol=1e-10, atol=1e-10)
+
+
+def test_survey_kat_point():
+    x = np.array([[.1, .2, .3, .4]]); u = np.array([[0, 1.5]])
+    np.testing.assert_allclose(onp.rk4(x, u)[0], [0.10557615, 0.20864331, 0.25800997, 0.46286099], atol=5e-9)
+    A, B = onp.jacobians(x, u)
+    np.testing.assert_allclose(A[0, 2], [-9.16176471, 3.89155693, -0.69518935, 1.70153563], atol=5e-8)
+    np.testing.assert_allclose(B[0, 2:, 1], [-1.58226365, 4.64323238], atol=5e-8)
+
+
+def test_c_oracle_primitives_match_reference(golden):
+    g = golden("kat_primitives")
+    for i in range(g["X"].shape[0]):
+        np.testing.assert_allclose(oc.rk4(g["X"][i], g["U"][i]), g["f_rk4"][i], rtol=1e-11, atol=1e-9)
+        A, B = oc.jacobians(g["X"][i], g["U"][i])
+        np.testing.assert_allclose(A, g["A_c"][i], rtol=1e-10, atol=1e-8)
+        np.testing.assert_allclose(B, g["B_c"][i], rtol=1e-10, atol=1e-12)
+
+
+# ------------------------------------------------------------------------ one Newton iteration
+@pytest.mark.parametrize("tag", ["it0", "mid"])
+def test_numpy_oracle_newton_iteration(golden, tag):
+    g = golden("newton_iteration")
+    x, u = g[f"{tag}_x"][None], g[f"{tag}_u"][None]
+    xr, ur = g["x_ref"], g["u_ref"]
+    lam = onp.costate(x, u, xr, ur)[0]
+    assert rel_l2(lam, g[f"{tag}_lambda"]) < 1e-12
+    Ad, Bd, q, r, QTb, qT = onp.stage_lists(x, u, xr, ur)
+    np.testing.assert_allclose(Ad[0], g[f"{tag}_A_d"], rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(Bd[0], g[f"{tag}_B_d"], rtol=1e-11, atol=1e-14)
+    np.testing.assert_allclose(q[0], g[f"{tag}_q"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(r[0], g[f"{tag}_r"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(qT[0], g[f"{tag}_qT"], rtol=1e-13)
+    K, sig, dJ = onp.riccati(Ad, Bd, 2 * onp.Q_DEFAULT, 2 * onp.R_DEFAULT, np.zeros((2, 4)), q, r, QTb, qT)
+    assert rel_l2(K[0], g[f"{tag}_K"]) < 1e-10
+    assert rel_l2(sig[0], g[f"{tag}_sigma"]) < 1e-10
+    assert dJ[0] == pytest.approx(float(g[f"{tag}_dJ"]), rel=1e-10)
+    assert np.all(K[0, :, 0, :] == 0)                     # K row 0 == 0
+    for gam, sfx in ((0.1, "01"), (1.0, "1")):
+        xn, un = onp.closed_loop(x, u, K, sig, gam)
+        assert rel_l2(xn[0], g[f"{tag}_xn{sfx}"]) < 1e-10
+        assert rel_l2(un[0], g[f"{tag}_un{sfx}"]) < 1e-10
+        J = onp.total_cost(xn, un, xr, ur)[0]
+        assert J == pytest.approx(float(g[f"{tag}_cost{sfx}"]), rel=1e-11)
+    assert onp.total_cost(x, u, xr, ur)[0] == pytest.approx(float(g[f"{tag}_cost"]), rel=1e-13)
+
+
+def test_numpy_oracle_general_riccati(golden):
+    g = golden("newton_iteration")
+    K, sig, dJ = onp.riccati(g["gen_A"][None], g["gen_B"][None], g["gen_Q"][None], g["gen_R"][None],
+                             g["gen_S"][None], g["gen_q"][None], g["gen_r"][None], g["gen_QT"], g["gen_qT"][None])
+    assert rel_l2(K[0], g["gen_K"]) < 1e-12
+    assert rel_l2(sig[0], g["gen_sigma"]) < 1e-12
+    assert dJ[0] == pytest.approx(float(g["gen_dJ"]), rel=1e-12)
+
+
+def test_numpy_oracle_open_loop(golden):
+    g = golden("newton_iteration")
+    x = onp.simulate_open_loop(g["sim_x0"][None], g["sim_u"][None])
+    assert rel_l2(x[0], g["sim_x"]) < 1e-12
+
+
+def test_numpy_oracle_newton_first_iterations(golden, task2_refs):
+    """The vectorised driver reproduces the reference's first 6 cost / sigma-norm values on 3 lanes."""
+    L = golden("lanes")
+    pick = [0, 6, 10]      # u05_s0, u15_s10 (backtracks later), upi_s12
+    xr, ur, _ = task2_refs
+    res = onp.newton_solve(L["x0"][pick], xr, ur, max_iters=6, tol=1e-4, gamma_0=0.1)
+    for j, i in enumerate(pick):
+        np.testing.assert_allclose(res["cost_hist"][:, j], L["cost_hist"][i, :7], rtol=1e-11)
+        np.testing.assert_allclose(res["sigma_norm_hist"][:, j], L["sigma_norm_hist"][i, :6], rtol=1e-9)
+
+
+# ----------------------------------------------------------------------------- full solves
+def test_c_oracle_task2_matches_reference_golden(golden, task2_refs):
+    xr, ur, _ = task2_refs
+    ref = golden("task2_reference_output")      # the reference's own committed output
+    run = golden("task2_solve")
+    r = oc.newton_solve(np.zeros((1, 4)), xr, ur, max_iters=5000, tol=1e-4, gamma_0=0.1)
+    assert int(r["n_iter"][0]) == int(run["n_iter"]) == 393
+    assert int(r["status"][0]) == onp.CONVERGED
+    assert rel_l2(r["x"][0], ref["x"]) < 1e-8
+    assert rel_l2(r["u"][0], ref["u"]) < 1e-8
+    assert r["cost"][0] == pytest.approx(28063.21834988144, rel=1e-10)
+    assert rel_l2(r["K"][0], run["K"]) < 1e-8
+    assert rel_l2(r["sigma"][0], run["sigma"]) < 1e-6
+
+
+def test_c_oracle_lanes_match_reference(golden, task2_refs):
+    L = golden("lanes")
+    xr, ur, _ = task2_refs
+    r = oc.newton_solve(L["x0"], xr, ur, max_iters=5000, tol=1e-4, gamma_0=0.1)
+    codes = {1: onp.CONVERGED, 2: onp.LS_FAILED}
+    for i, name in enumerate(L["names"]):
+        assert int(r["n_iter"][i]) == int(L["n_iter"][i]), name
+        assert int(r["status"][i]) == codes[int(L["status"][i])], name
+        assert rel_l2(r["x"][i], L["x"][i]) < 1e-8, name
+        assert rel_l2(r["u"][i], L["u"][i]) < 1e-8, name
+
+
+def test_c_oracle_task1_matches_reference(golden):
+    g = golden("task1_solve")
+    r = oc.newton_solve(g["x0"][None], g["x_ref"], g["u_ref_full"], max_iters=5000, tol=1e-4, gamma_0=0.05)
+    assert int(r["n_iter"][0]) == int(g["n_iter"]) == 173
+    assert rel_l2(r["x"][0], g["x"]) < 1e-8
+    assert rel_l2(r["u"][0], g["u"]) < 1e-8
+    assert np.abs(r["u"][0, :, 0]).max() > 0.1          # the tau1 channel is live in task 1
