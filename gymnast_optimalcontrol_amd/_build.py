@@ -37,17 +37,19 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Compile the library (``out`` and ``defines`` build A/B variants for measurement)."""
+    target = out or LIB_PATH
+    if out is None and not force and not needs_build():
         return LIB_PATH
-    tmp = LIB_PATH + ".tmp"
+    tmp = target + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
+           *[f"-D{d}" for d in defines], "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

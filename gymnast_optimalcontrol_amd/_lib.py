@@ -21,7 +21,7 @@ EXPORTS = (
     "gym_pack_lanes", "gym_unpack_lanes", "gym_unpack_gains",
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
     "gym_riccati_general",
-    "gym_newton_init", "gym_newton_iteration", "gym_newton_finalize",
+    "gym_newton_init", "gym_newton_iteration", "gym_newton_finalize", "gym_newton_sigma",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats")
@@ -53,7 +53,7 @@ class GymTiming(C.Structure):
 
 class GymBatch(C.Structure):
     _fields_ = [("B", C.c_int64), ("Bp", C.c_int64), ("N", C.c_int32), ("hist_len", C.c_int32),
-                ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("sigma", _P), ("x_ref", _P), ("u_ref", _P),
+                ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("cs", _P), ("x_ref", _P), ("u_ref", _P),
                 ("cost", _P), ("dJ", _P), ("smax", _P), ("gamma", _P), ("status", _P), ("n_iter", _P),
                 ("res_buf", _P), ("n_roll", _P), ("retry_list", _P), ("counters", _P), ("cand_ok", _P),
                 ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P),
@@ -69,8 +69,8 @@ _SIGS = {
     "gym_rk4_step": [_MP, _P, _P, _P, _I64, _P],
     "gym_jacobians": [_MP, _P, _P, _P, _P, _I64, _P],
     "gym_stage_cost_derivs": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _P],
-    "gym_pack_lanes": [_P, _P, _I64, _I64, _I32, _I32, _P],
-    "gym_unpack_lanes": [_P, _P, _P, _P, _I64, _I64, _I32, _I32, _P],
+    "gym_pack_lanes": [_P, _P, _I64, _I64, _I32, _I32, _I32, _P],
+    "gym_unpack_lanes": [_P, _P, _P, _P, _I64, _I64, _I32, _I32, _I32, _P],
     "gym_unpack_gains": [_P, _P, _I64, _I64, _I32, _P],
     "gym_rollout_open_loop": [_MP, _WP, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
     "gym_closed_loop": [_MP, _WP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _P],
@@ -80,19 +80,19 @@ _SIGS = {
     "gym_riccati_general": [_P] * 12 + [_I64, _I64, _I32, _P],
     "gym_newton_init": [_MP, _WP, _P, _BP, _P],
     "gym_newton_iteration": [_MP, _WP, _AP, _BP, _I32, _P],
-    "gym_newton_finalize": [_BP, _I32, _P, _P, _P, _P, _P],
+    "gym_newton_finalize": [_WP, _BP, _I32, _P, _P, _P, _P, _P],
+    "gym_newton_sigma": [_WP, _BP, _P, _P],
     "gym_timing_create": [C.POINTER(GymTiming)],
     "gym_timing_destroy": [C.POINTER(GymTiming)],
     "gym_timing_collect": [C.POINTER(GymTiming)],
 }
 
-_lib = None
+_libs: dict = {}
 
 
 def load(path: str = LIB_PATH):
-    """Load (once) and return the ctypes library.  Raises if the HIP library is not built."""
-    global _lib
-    if _lib is None:
+    """Load (once per path) and return the ctypes library.  Raises if the HIP library is not built."""
+    if path not in _libs:
         if not os.path.exists(path):
             raise ImportError(
                 f"{path} is missing: build the HIP library first (python -m gymnast_optimalcontrol_amd._build "
@@ -102,8 +102,8 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = C.c_int
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 def check(rc: int, what: str):
@@ -111,12 +111,12 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed with HIP error code {rc}")
 
 
-def require_device(device=None) -> torch.device:
+def require_device(device=None, lib_path: str = LIB_PATH) -> torch.device:
     """The compute path runs on a HIP device only."""
     if not torch.cuda.is_available():
         raise RuntimeError("gymnast_optimalcontrol_amd needs a HIP (ROCm) GPU: no device is visible "
                            "and there is no CPU fallback")
-    load()
+    load(lib_path)
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     if dev.type != "cuda":
         raise ValueError(f"device must be a HIP device, got {dev}")

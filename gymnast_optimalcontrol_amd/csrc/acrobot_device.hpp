@@ -20,34 +20,124 @@ struct Dyn {
           f2(m.f2), h(m.dt), h2(m.dt * 0.5), h6(1.0 / 6.0) {}
 };
 
+// ------------------------------------------------------------------------------------------
+// fp64 sin/cos for the arguments this model produces.  ocml's sincos carries the reduced
+// argument as a double-double and a Payne-Hanek path (~60-75 VALU per call); the angles of an
+// acrobot trajectory are moderate, so a 2-term Cody-Waite reduction with FMA (exact first step
+// for |k| < 2^20) and the fdlibm minimax kernels on [-pi/4, pi/4] give the same absolute accuracy
+// (~1.5 ulp absolute, checked against long-double sin/cos) in ~30 instructions.
+// Domain: |x| < 2^20 * pi/2 ~ 1.6e6 rad.  Beyond it (or for inf/NaN) both results are NaN: a lane
+// whose joint angle has reached 2.5e5 revolutions has diverged (RK4 at dt = 0.02 is unstable long
+// before), and NaN makes its cost NaN so the Armijo test fails exactly as the reference's does for
+// a non-finite trajectory.  Keeping ocml's full-range path out of the kernels saves ~25 VGPRs.
+// ------------------------------------------------------------------------------------------
+// fdlibm minimax kernels: sin(r), cos(r) for |r| <= pi/4.
+__device__ __forceinline__ double ksin(double r, double z) {
+    return fma(r * z, fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+        2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
+        -1.66666666666666324348e-01), r);
+}
+__device__ __forceinline__ double kcos(double z) {
+    return fma(z * z, fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+        -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
+        4.16666666666666019037e-02), fma(-0.5, z, 1.0));
+}
+
+__device__ __forceinline__ void fast_sincos(double x, double* s, double* c) {
+    constexpr double kTwoOverPi = 6.36619772367581382433e-01;
+    constexpr double kPio2Hi = 1.57079632679489655800e+00;   // 0x3FF921FB54442D18
+    constexpr double kPio2Lo = 6.12323399573676603587e-17;   // 0x3C91A62633145C07
+    const double kq = __builtin_rint(x * kTwoOverPi);
+    const double qn = (fabs(kq) < 1048576.0) ? kq : __builtin_nan("");   // outside the domain: NaN
+    const double r = fma(-qn, kPio2Lo, fma(-qn, kPio2Hi, x));
+    const double z = r * r;
+    const double sr = ksin(r, z);
+    const double cr = kcos(z);
+    const int q = (int)qn;                 // v_cvt_i32_f64 maps NaN to 0
+    const double ss = (q & 1) ? cr : sr;   // quadrant rotation
+    const double cc = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// 1/v for v in the well-conditioned range of det M: hardware reciprocal + two Newton steps.
+__device__ __forceinline__ double recip(double v) {
+    double r = __builtin_amdgcn_rcp(v);
+    double e = fma(-v, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-v, r, 1.0);
+    return fma(r, e, r);
+}
+
 // Joint accelerations qdd = M(th2)^-1 (tau - (C+F) w - G), tau = [0, tau2]   (dynamics.py:197-213,
 // M/C/G/F of dynamics.py:63-90).  det M = d (a - d) - b^2 cos^2(th2) > 0 is formed without cancellation.
 __device__ __forceinline__ void accel(const Dyn& m, double th1, double th2, double w1, double w2, double tau2,
                                       double& q1, double& q2) {
     double s1, c1, s2, c2;
-    sincos(th1, &s1, &c1);
-    sincos(th2, &s2, &c2);
+    fast_sincos(th1, &s1, &c1);
+    fast_sincos(th2, &s2, &c2);
     const double s12 = s1 * c2 + c1 * s2;            // sin(th1 + th2)
     const double bs2 = m.b * s2;
     const double M11 = m.a2b + 2.0 * m.b * c2;
     const double M12 = m.d + m.b * c2;
     const double r1 = bs2 * w2 * (2.0 * w1 + w2) - m.f1 * w1 - (m.g1 * s1 + m.g2 * s12);
     const double r2 = tau2 - bs2 * w1 * w1 - m.f2 * w2 - m.g2 * s12;
-    const double inv = 1.0 / (m.dad - m.bb * (c2 * c2));
+    const double inv = recip(m.dad - m.bb * (c2 * c2));
     q1 = (m.d * r1 - M12 * r2) * inv;
     q2 = (M11 * r2 - M12 * r1) * inv;
 }
 
-// Classic RK4 with the control held over the step (dynamics.py:177-195), in place.
+// accel() from precomputed sin/cos of both joint angles.
+__device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, double s2, double c2, double w1,
+                                         double w2, double tau2, double& q1, double& q2) {
+    const double s12 = s1 * c2 + c1 * s2;            // sin(th1 + th2)
+    const double bs2 = m.b * s2;
+    const double M11 = m.a2b + 2.0 * m.b * c2;
+    const double M12 = m.d + m.b * c2;
+    const double r1 = bs2 * w2 * (2.0 * w1 + w2) - m.f1 * w1 - (m.g1 * s1 + m.g2 * s12);
+    const double r2 = tau2 - bs2 * w1 * w1 - m.f2 * w2 - m.g2 * s12;
+    const double inv = recip(m.dad - m.bb * (c2 * c2));
+    q1 = (m.d * r1 - M12 * r2) * inv;
+    q2 = (M11 * r2 - M12 * r1) * inv;
+}
+
+// sin/cos of th + d from sin/cos of th (angle addition; d is an RK4 sub-step displacement, so
+// |d| <= pi/4 unless |w| > 39 rad/s, in which case the argument is reduced from scratch).
+#ifndef GYM_RK4_ROTATE
+#define GYM_RK4_ROTATE 0
+#endif
+__device__ __forceinline__ void rotate(double th, double d, double s, double c, double& so, double& co) {
+    if (GYM_RK4_ROTATE && __builtin_expect(fabs(d) <= 0.78539816339744830962, 1)) {
+        const double z = d * d;
+        const double sd = ksin(d, z), cd = kcos(z);
+        so = fma(s, cd, c * sd);
+        co = fma(c, cd, -(s * sd));
+    } else {
+        fast_sincos(th + d, &so, &co);
+    }
+}
+
+// Classic RK4 with the control held over the step (dynamics.py:177-195), in place.  The angles of
+// the three sub-step states are x + d with d = (h/2) k1, (h/2) k2, h k3; their sin/cos come from
+// angle addition on the step's base angles, so only the base angles need an argument reduction.
 __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2) {
     double a1, b1, a2, b2, a3, b3, a4, b4;
-    accel(m, x0, x1, x2, x3, tau2, a1, b1);                       // k1 = (x2, x3, a1, b1)
-    const double y0 = x0 + m.h2 * x2, y1 = x1 + m.h2 * x3, y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
-    accel(m, y0, y1, y2, y3, tau2, a2, b2);                       // k2 = (y2, y3, a2, b2)
-    const double z0 = x0 + m.h2 * y2, z1 = x1 + m.h2 * y3, z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
-    accel(m, z0, z1, z2, z3, tau2, a3, b3);                       // k3 = (z2, z3, a3, b3)
-    const double v0 = x0 + m.h * z2, v1 = x1 + m.h * z3, v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
-    accel(m, v0, v1, v2, v3, tau2, a4, b4);                       // k4 = (v2, v3, a4, b4)
+    double s1, c1, s2, c2, t1, u1, t2, u2;
+    fast_sincos(x0, &s1, &c1);
+    fast_sincos(x1, &s2, &c2);
+    accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
+    const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
+    rotate(x0, m.h2 * x2, s1, c1, t1, u1);
+    rotate(x1, m.h2 * x3, s2, c2, t2, u2);
+    accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
+    const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
+    rotate(x0, m.h2 * y2, s1, c1, t1, u1);
+    rotate(x1, m.h2 * y3, s2, c2, t2, u2);
+    accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
+    const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
+    rotate(x0, m.h * z2, s1, c1, t1, u1);
+    rotate(x1, m.h * z3, s2, c2, t2, u2);
+    accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
     const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
     const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;
     const double n2 = x2 + (m.h * (((a1 + 2.0 * a2) + 2.0 * a3) + a4)) * m.h6;
@@ -63,14 +153,14 @@ struct Jac {
 
 __device__ __forceinline__ Jac jacobian(const Dyn& m, double th1, double th2, double w1, double w2, double tau2) {
     double s1, c1, s2, c2;
-    sincos(th1, &s1, &c1);
-    sincos(th2, &s2, &c2);
+    fast_sincos(th1, &s1, &c1);
+    fast_sincos(th2, &s2, &c2);
     const double s12 = s1 * c2 + c1 * s2, c12 = c1 * c2 - s1 * s2;
     const double bs2 = m.b * s2, bc2 = m.b * c2;
     const double M11 = m.a2b + 2.0 * bc2, M12 = m.d + bc2;
     const double r1 = bs2 * w2 * (2.0 * w1 + w2) - m.f1 * w1 - (m.g1 * s1 + m.g2 * s12);
     const double r2 = tau2 - bs2 * w1 * w1 - m.f2 * w2 - m.g2 * s12;
-    const double inv = 1.0 / (m.dad - m.bb * (c2 * c2));
+    const double inv = recip(m.dad - m.bb * (c2 * c2));
     const double q1 = (m.d * r1 - M12 * r2) * inv, q2 = (M11 * r2 - M12 * r1) * inv;
     // d qdd / d x_j = M^-1 (d r/d x_j - (d M/d x_j) qdd);  only dM/dth2 != 0.
     const double gc = m.g2 * c12;

@@ -1,11 +1,18 @@
 // MI355X (gfx950) kernels + C-ABI of the batched acrobot Newton/Armijo engine.
 //
 // One trajectory ("lane") per GPU thread, 64-thread workgroups (one wavefront), time-major SoA
-// streams with the lane innermost and two fp64 components per 16-byte element, so every
-// per-stage load/store of a wavefront is one contiguous 1 KiB transaction.  The shared
-// references x_ref (N,4), u_ref (T,2) are read with wave-uniform addresses (scalar loads).
-// The whole per-lane recursion (Jacobians, Riccati state P/p, RK4 state, running cost) is
-// register-resident; no LDS is needed because lanes never exchange data.
+// streams with the lane innermost.  States and gains are stored as 16-byte pairs (one 1 KiB
+// transaction per wavefront load), controls and sigma as 8-byte planes.  The shared references
+// x_ref (N,4), u_ref (T,2) are read with wave-uniform addresses (scalar loads).  The whole
+// per-lane recursion (Jacobians, Riccati state P/p, RK4 state, running cost) is register-resident;
+// no LDS is needed because lanes never exchange data.
+//
+// The solver's two HBM streams per Newton iteration:
+//   backward sweep : read x (2 pairs) + u (2 planes), write K row 1 (2 pairs) + (c1, sigma1) (1 pair)
+//   Armijo trial   : read K row 1 + (c1, sigma1) + u0, write x_new (2 pairs) + u_new (2 planes)
+// where c1 = u1 - K1 x folds the reference's u1 + K1 (x_new - x) into c1 + K1 x_new, so the trial
+// never re-reads the old trajectory x; sigma0 = -r0 / (2 R0) is recomputed from u0 bit-identically.
+// Streamed once per pass, these use non-temporal loads/stores.
 //
 // Reference: /root/reference/trajectory_generation.py (newton_Algorithm :298-398 and the
 // primitives it calls) and dynamics.py.  See include/gymnast_acrobot.h for the ABI.
@@ -25,7 +32,7 @@ constexpr int STAT_BLOCKS = 256;  // first stage of the deterministic statistics
 constexpr int STAT_THREADS = 256;
 constexpr int NSTAT = 8;
 
-enum KMode { K_OPEN = 0, K_COMPACT = 1, K_FULL = 2 };
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 inline int grid_for(int64_t n, int block, int64_t cap = (int64_t)1 << 30) {
     int64_t g = (n + block - 1) / block;
@@ -34,81 +41,122 @@ inline int grid_for(int64_t n, int block, int64_t cap = (int64_t)1 << 30) {
     return (int)g;
 }
 
+// streamed (read-once / write-once per pass) accesses: non-temporal
+__device__ __forceinline__ double2 ld_nt(const double2* p) {
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ double ld_nt(const double* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(double2* p, double a, double b) {
+    d2v v = {a, b};
+    __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(p));
+}
+__device__ __forceinline__ void st_nt(double* p, double a) { __builtin_nontemporal_store(a, p); }
+
+// element index of (t, component-group p of P, lane) in a time-major SoA stream
+__device__ __forceinline__ int64_t pix(int t, int p, int P, int64_t l, int64_t Bp) { return ((int64_t)t * P + p) * Bp + l; }
+
+// stage cost exactly as total_cost accumulates it (:244-245): J += dx^T Q dx ; J += du^T R du
+__device__ __forceinline__ double xcost(const double* w, double n0, double n1, double n2, double n3,
+                                        const double* xr) {
+    const double e0 = n0 - xr[0], e1 = n1 - xr[1], e2 = n2 - xr[2], e3 = n3 - xr[3];
+    return ((e0 * (w[0] * e0) + e1 * (w[1] * e1)) + e2 * (w[2] * e2)) + e3 * (w[3] * e3);
+}
+
 // ------------------------------------------------------------------------------------------
-// Closed-loop / open-loop rollout of one lane with its total cost fused in
-// (forward_closed_loop_update :218-229 + total_cost :231-252; simulate_open_loop :74-87).
+// Reference-form rollouts (forward_closed_loop_update :218-229 + total_cost :231-252;
+// simulate_open_loop :74-87) for the API entry points:
 //   u_new_t = u_t + K_t (x_new_t - x_t) + gamma sigma_t ;  x_new_{t+1} = RK4(x_new_t, u_new_t)
-// KM = K_OPEN: u_new_t = u_t (no feedback).  Stage cost accumulated as the reference does:
-// J += dx^T Q dx ; J += du^T R du  per stage, then + dx_N^T Q_T dx_N.
+// FULLK = false: open loop, u_new_t = u_t.  x pairs (N,2,Bp); u, sigma planes (T,2,Bp); K pairs (T,4,Bp).
 // ------------------------------------------------------------------------------------------
-template <int KM, bool WRITE>
-__device__ __forceinline__ double rollout(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
-                                          const double2* __restrict__ u, const double2* __restrict__ K,
-                                          const double2* __restrict__ s, const double* __restrict__ xr,
-                                          const double* __restrict__ ur, double2* __restrict__ xn,
-                                          double2* __restrict__ un, double gamma, int64_t l, int64_t Bp, int N,
-                                          double n0, double n1, double n2, double n3) {
+template <bool FULLK>
+__device__ __forceinline__ double rollout_ref(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+                                              const double* __restrict__ u, const double2* __restrict__ K,
+                                              const double* __restrict__ s, const double* __restrict__ xr,
+                                              const double* __restrict__ ur, double2* __restrict__ xn,
+                                              double* __restrict__ un, double gamma, int64_t l, int64_t Bp, int N,
+                                              double n0, double n1, double n2, double n3) {
     const int T = N - 1;
-    constexpr int KP = (KM == K_FULL) ? 4 : 2;  // double2 pairs of gains per stage
+    double J = 0.0;
+    xn[l] = make_double2(n0, n1);
+    xn[Bp + l] = make_double2(n2, n3);
+    for (int t = 0; t < T; ++t) {
+        double v0 = u[pix(t, 0, 2, l, Bp)], v1 = u[pix(t, 1, 2, l, Bp)];
+        if (FULLK) {
+            const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
+            const double2 k0 = K[pix(t, 0, 4, l, Bp)], k1 = K[pix(t, 1, 4, l, Bp)];
+            const double2 k2 = K[pix(t, 2, 4, l, Bp)], k3 = K[pix(t, 3, 4, l, Bp)];
+            const double d0 = n0 - a.x, d1 = n1 - a.y, d2 = n2 - b.x, d3 = n3 - b.y;
+            const double kd0 = ((k0.x * d0 + k0.y * d1) + k1.x * d2) + k1.y * d3;
+            const double kd1 = ((k2.x * d0 + k2.y * d1) + k3.x * d2) + k3.y * d3;
+            v0 = (v0 + kd0) + gamma * s[pix(t, 0, 2, l, Bp)];
+            v1 = (v1 + kd1) + gamma * s[pix(t, 1, 2, l, Bp)];
+            un[pix(t, 0, 2, l, Bp)] = v0;
+            un[pix(t, 1, 2, l, Bp)] = v1;
+        }
+        const double* urt = ur + 2 * t;
+        const double f0 = v0 - urt[0], f1 = v1 - urt[1];
+        J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
+        J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
+        gym::rk4(m, n0, n1, n2, n3, v1);
+        xn[pix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
+        xn[pix(t + 1, 1, 2, l, Bp)] = make_double2(n2, n3);
+    }
+    return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
+}
+
+// ------------------------------------------------------------------------------------------
+// Solver rollout (Armijo trial / candidate / accepted-candidate re-run), offset form:
+//   u_new0 = u0 + gamma sigma0,  sigma0 = -(2R0 (u0 - ur0)) / (2R0)     (bit-identical to the sweep)
+//   u_new1 = (c1 + K1 x_new) + gamma sigma1,  c1 = u1 - K1 x  (the sweep's offset)
+// Streams per stage: K1 (2 pairs) + (c1, sigma1) (1 pair) + u0 (plane) in; x_new, u_new out.
+// ------------------------------------------------------------------------------------------
+template <bool WRITE>
+__device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights& w, const double* __restrict__ u,
+                                                const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                const double* __restrict__ xr, const double* __restrict__ ur,
+                                                double2* __restrict__ xn, double* __restrict__ un, double gamma,
+                                                int64_t l, int64_t Bp, int N, double n0, double n1, double n2,
+                                                double n3) {
+    const int T = N - 1;
+    const double G00 = 2.0 * w.R[0], iG00 = 1.0 / G00;
     double J = 0.0;
     if (WRITE) {
-        xn[l] = make_double2(n0, n1);
-        xn[Bp + l] = make_double2(n2, n3);
+        st_nt(&xn[l], n0, n1);
+        st_nt(&xn[Bp + l], n2, n3);
     }
     // software prefetch of stage t+1's streams while stage t computes
-    double2 pa = make_double2(0, 0), pb = pa, pu, ps = pa, pk[KP];
-    auto load = [&](int t) {
-        pu = u[(int64_t)t * Bp + l];
-        if (KM != K_OPEN) {
-            pa = x[((int64_t)t * 2 + 0) * Bp + l];
-            pb = x[((int64_t)t * 2 + 1) * Bp + l];
-#pragma unroll
-            for (int p = 0; p < KP; ++p) pk[p] = K[((int64_t)t * KP + p) * Bp + l];
-            ps = s[(int64_t)t * Bp + l];
-        }
-    };
-    load(0);
+    double2 pk0 = ld_nt(&K1[pix(0, 0, 2, l, Bp)]), pk1 = ld_nt(&K1[pix(0, 1, 2, l, Bp)]);
+    double2 pc = ld_nt(&cs[l]);
+    double pu0 = ld_nt(&u[l]);
     for (int t = 0; t < T; ++t) {
-        const double2 ca = pa, cb = pb, cu = pu, cs = ps;
-        double2 ck[KP];
-#pragma unroll
-        for (int p = 0; p < KP; ++p) ck[p] = pk[p];
-        if (t + 1 < T) load(t + 1);
-        double v0, v1;
-        if (KM == K_OPEN) {
-            v0 = cu.x;
-            v1 = cu.y;
-        } else {
-            const double d0 = n0 - ca.x, d1 = n1 - ca.y, d2 = n2 - cb.x, d3 = n3 - cb.y;
-            if (KM == K_COMPACT) {
-                // K_t row 0 is identically zero (B_c[:,0] == 0, G diagonal): u0 + 0 + gamma sigma0
-                const double kd1 = ((ck[0].x * d0 + ck[0].y * d1) + ck[1].x * d2) + ck[1].y * d3;
-                v0 = cu.x + gamma * cs.x;
-                v1 = (cu.y + kd1) + gamma * cs.y;
-            } else {
-                const double kd0 = ((ck[0].x * d0 + ck[0].y * d1) + ck[1].x * d2) + ck[1].y * d3;
-                const double kd1 = ((ck[2].x * d0 + ck[2].y * d1) + ck[3].x * d2) + ck[3].y * d3;
-                v0 = (cu.x + kd0) + gamma * cs.x;
-                v1 = (cu.y + kd1) + gamma * cs.y;
-            }
+        const double2 k0 = pk0, k1 = pk1, c = pc;
+        const double u0 = pu0;
+        if (t + 1 < T) {
+            pk0 = ld_nt(&K1[pix(t + 1, 0, 2, l, Bp)]);
+            pk1 = ld_nt(&K1[pix(t + 1, 1, 2, l, Bp)]);
+            pc = ld_nt(&cs[(int64_t)(t + 1) * Bp + l]);
+            pu0 = ld_nt(&u[pix(t + 1, 0, 2, l, Bp)]);
         }
-        const double* xrt = xr + 4 * t;
         const double* urt = ur + 2 * t;
-        const double e0 = n0 - xrt[0], e1 = n1 - xrt[1], e2 = n2 - xrt[2], e3 = n3 - xrt[3];
+        const double s0 = -(G00 * (u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
+        const double v0 = u0 + gamma * s0;
+        const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
+        const double v1 = (c.x + kx) + gamma * c.y;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
-        J += ((e0 * (w.Q[0] * e0) + e1 * (w.Q[1] * e1)) + e2 * (w.Q[2] * e2)) + e3 * (w.Q[3] * e3);
+        J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
         J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
-        if (WRITE) un[(int64_t)t * Bp + l] = make_double2(v0, v1);
+        if (WRITE) {
+            st_nt(&un[pix(t, 0, 2, l, Bp)], v0);
+            st_nt(&un[pix(t, 1, 2, l, Bp)], v1);
+        }
         gym::rk4(m, n0, n1, n2, n3, v1);
         if (WRITE) {
-            xn[((int64_t)(t + 1) * 2 + 0) * Bp + l] = make_double2(n0, n1);
-            xn[((int64_t)(t + 1) * 2 + 1) * Bp + l] = make_double2(n2, n3);
+            st_nt(&xn[pix(t + 1, 0, 2, l, Bp)], n0, n1);
+            st_nt(&xn[pix(t + 1, 1, 2, l, Bp)], n2, n3);
         }
     }
-    const double* xrT = xr + 4 * T;
-    const double e0 = n0 - xrT[0], e1 = n1 - xrT[1], e2 = n2 - xrT[2], e3 = n3 - xrT[3];
-    J += ((e0 * (w.QT[0] * e0) + e1 * (w.QT[1] * e1)) + e2 * (w.QT[2] * e2)) + e3 * (w.QT[3] * e3);
-    return J;
+    return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -117,19 +165,21 @@ __device__ __forceinline__ double rollout(const Dyn& m, const gym_weights& w, co
 //   A_d = I + dt A_c with A_c rows 0,1 = e3^T, e4^T ; B_d = dt B_c with only column 1 non-zero
 //   Q_t = 2Q, R_t = 2R (diagonal), S_t = 0  =>  G = diag(2R0, 2R1 + b^T P b), K_t row 0 = 0.
 // P is kept symmetric (10 registers), p and (optionally) the costate lambda in registers.
+// SOLVER: writes K1 and (c1 = u1 - K1 x, sigma1); API: writes K1 and sigma planes (+ lambda).
 // ------------------------------------------------------------------------------------------
-template <bool LAMBDA>
+template <bool SOLVER, bool LAMBDA>
 __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
-                                              const double2* __restrict__ u, const double* __restrict__ xr,
+                                              const double* __restrict__ u, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ K1,
-                                              double2* __restrict__ sig, double2* __restrict__ lam, int64_t l,
-                                              int64_t Bp, int N, double& dJ_out, double& smax_out) {
+                                              double2* __restrict__ cs, double* __restrict__ sig,
+                                              double2* __restrict__ lam, int64_t l, int64_t Bp, int N,
+                                              double& dJ_out, double& smax_out) {
     const int T = N - 1;
     const double dt = m.h;
     double P00, P01, P02, P03, P11, P12, P13, P22, P23, P33, p0, p1, p2, p3;
     double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     {
-        const double2 xa = x[((int64_t)T * 2 + 0) * Bp + l], xb = x[((int64_t)T * 2 + 1) * Bp + l];
+        const double2 xa = x[pix(T, 0, 2, l, Bp)], xb = x[pix(T, 1, 2, l, Bp)];
         const double* xrT = xr + 4 * T;
         P00 = 2.0 * w.QT[0]; P11 = 2.0 * w.QT[1]; P22 = 2.0 * w.QT[2]; P33 = 2.0 * w.QT[3];
         P01 = P02 = P03 = P12 = P13 = P23 = 0.0;
@@ -137,23 +187,25 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         p2 = P22 * (xb.x - xrT[2]); p3 = P33 * (xb.y - xrT[3]);
         if (LAMBDA) {
             l0 = p0; l1 = p1; l2 = p2; l3 = p3;
-            lam[((int64_t)T * 2 + 0) * Bp + l] = make_double2(l0, l1);
-            lam[((int64_t)T * 2 + 1) * Bp + l] = make_double2(l2, l3);
+            lam[pix(T, 0, 2, l, Bp)] = make_double2(l0, l1);
+            lam[pix(T, 1, 2, l, Bp)] = make_double2(l2, l3);
         }
     }
     const double twoQ0 = 2.0 * w.Q[0], twoQ1 = 2.0 * w.Q[1], twoQ2 = 2.0 * w.Q[2], twoQ3 = 2.0 * w.Q[3];
-    const double G00 = 2.0 * w.R[0], twoR1 = 2.0 * w.R[1];
+    const double G00 = 2.0 * w.R[0], twoR1 = 2.0 * w.R[1], iG00 = 1.0 / G00;
     double dJ = 0.0, smax = 0.0;
-    double2 pa = x[((int64_t)(T - 1) * 2 + 0) * Bp + l], pb = x[((int64_t)(T - 1) * 2 + 1) * Bp + l];
-    double2 pu = u[(int64_t)(T - 1) * Bp + l];
+    double2 pa = ld_nt(&x[pix(T - 1, 0, 2, l, Bp)]), pb = ld_nt(&x[pix(T - 1, 1, 2, l, Bp)]);
+    double pu0 = ld_nt(&u[pix(T - 1, 0, 2, l, Bp)]), pu1 = ld_nt(&u[pix(T - 1, 1, 2, l, Bp)]);
     for (int t = T - 1; t >= 0; --t) {
-        const double2 xa = pa, xb = pb, ut = pu;
+        const double2 xa = pa, xb = pb;
+        const double ut0 = pu0, ut1 = pu1;
         if (t > 0) {
-            pa = x[((int64_t)(t - 1) * 2 + 0) * Bp + l];
-            pb = x[((int64_t)(t - 1) * 2 + 1) * Bp + l];
-            pu = u[(int64_t)(t - 1) * Bp + l];
+            pa = ld_nt(&x[pix(t - 1, 0, 2, l, Bp)]);
+            pb = ld_nt(&x[pix(t - 1, 1, 2, l, Bp)]);
+            pu0 = ld_nt(&u[pix(t - 1, 0, 2, l, Bp)]);
+            pu1 = ld_nt(&u[pix(t - 1, 1, 2, l, Bp)]);
         }
-        const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut.y);
+        const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1);
         // A_d rows 2,3 (rows 0,1 = [1 0 dt 0], [0 1 0 dt]); B_d = dt * [0 0 bc2 bc3]^T in column 1
         const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
         const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
@@ -162,15 +214,15 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         const double* urt = ur + 2 * t;
         const double q0 = twoQ0 * (xa.x - xrt[0]), q1 = twoQ1 * (xa.y - xrt[1]);
         const double q2 = twoQ2 * (xb.x - xrt[2]), q3 = twoQ3 * (xb.y - xrt[3]);
-        const double r0 = G00 * (ut.x - urt[0]), r1 = twoR1 * (ut.y - urt[1]);
+        const double r0 = G00 * (ut0 - urt[0]), r1 = twoR1 * (ut1 - urt[1]);
         if (LAMBDA) {  // lambda_t = 2Q dx_t + A_d^T lambda_{t+1}
             const double n0 = q0 + (l0 + A20 * l2 + A30 * l3);
             const double n1 = q1 + (l1 + A21 * l2 + A31 * l3);
             const double n2 = q2 + (dt * l0 + A22 * l2 + A32 * l3);
             const double n3 = q3 + (dt * l1 + A23 * l2 + A33 * l3);
             l0 = n0; l1 = n1; l2 = n2; l3 = n3;
-            lam[((int64_t)t * 2 + 0) * Bp + l] = make_double2(l0, l1);
-            lam[((int64_t)t * 2 + 1) * Bp + l] = make_double2(l2, l3);
+            lam[pix(t, 0, 2, l, Bp)] = make_double2(l0, l1);
+            lam[pix(t, 1, 2, l, Bp)] = make_double2(l2, l3);
         }
         // Pb = P B_d[:,1]
         const double Pb0 = P02 * bd2 + P03 * bd3, Pb1 = P12 * bd2 + P13 * bd3;
@@ -184,7 +236,7 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         const double g1 = r1 + (bd2 * p2 + bd3 * p3);
         const double iG = 1.0 / G11;
         const double k0 = -F0 * iG, k1 = -F1 * iG, k2 = -F2 * iG, k3 = -F3 * iG;
-        const double s0 = -r0 / G00, s1 = -g1 * iG;
+        const double s0 = -r0 * iG00, s1 = -g1 * iG;
         dJ += r0 * s0 + g1 * s1;
         // W = P A_d
         const double W00 = P00 + P02 * A20 + P03 * A30, W01 = P01 + P02 * A21 + P03 * A31;
@@ -216,9 +268,17 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         P00 = nP00; P01 = nP01; P02 = nP02; P03 = nP03; P11 = nP11; P12 = nP12; P13 = nP13;
         P22 = nP22; P23 = nP23; P33 = nP33;
         p0 = np0; p1 = np1; p2 = np2; p3 = np3;
-        K1[((int64_t)t * 2 + 0) * Bp + l] = make_double2(k0, k1);
-        K1[((int64_t)t * 2 + 1) * Bp + l] = make_double2(k2, k3);
-        sig[(int64_t)t * Bp + l] = make_double2(s0, s1);
+        if (SOLVER) {
+            const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
+            st_nt(&K1[pix(t, 0, 2, l, Bp)], k0, k1);
+            st_nt(&K1[pix(t, 1, 2, l, Bp)], k2, k3);
+            st_nt(&cs[(int64_t)t * Bp + l], c1, s1);
+        } else {
+            K1[pix(t, 0, 2, l, Bp)] = make_double2(k0, k1);
+            K1[pix(t, 1, 2, l, Bp)] = make_double2(k2, k3);
+            sig[pix(t, 0, 2, l, Bp)] = s0;
+            sig[pix(t, 1, 2, l, Bp)] = s1;
+        }
         smax = gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
     }
     dJ_out = dJ;
@@ -229,9 +289,9 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
 // kernels: API primitives
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights w, const double2* __restrict__ x,
-                                                      const double2* __restrict__ u, const double* __restrict__ xr,
+                                                      const double* __restrict__ u, const double* __restrict__ xr,
                                                       const double* __restrict__ ur, double2* __restrict__ K1,
-                                                      double2* __restrict__ sig, double* __restrict__ dJ,
+                                                      double* __restrict__ sig, double* __restrict__ dJ,
                                                       double* __restrict__ smax, double2* __restrict__ lam, int64_t B,
                                                       int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -239,37 +299,36 @@ __global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights 
     const Dyn m(mm);
     double d, s;
     if (lam)
-        backward_lane<true>(m, w, x, u, xr, ur, K1, sig, lam, l, Bp, N, d, s);
+        backward_lane<false, true>(m, w, x, u, xr, ur, K1, nullptr, sig, lam, l, Bp, N, d, s);
     else
-        backward_lane<false>(m, w, x, u, xr, ur, K1, sig, lam, l, Bp, N, d, s);
+        backward_lane<false, false>(m, w, x, u, xr, ur, K1, nullptr, sig, nullptr, l, Bp, N, d, s);
     if (dJ) dJ[l] = d;
     if (smax) smax[l] = s;
 }
 
 __global__ __launch_bounds__(BLK) void k_open_loop(gym_model mm, gym_weights w, const double* __restrict__ x0,
-                                                   const double2* __restrict__ u, const double* __restrict__ xr,
+                                                   const double* __restrict__ u, const double* __restrict__ xr,
                                                    const double* __restrict__ ur, double2* __restrict__ xn,
                                                    double* __restrict__ cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
     const Dyn m(mm);
-    const double J = rollout<K_OPEN, true>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
-                                           x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
+    const double J = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
+                                        x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
     if (cost) cost[l] = J;
 }
 
 __global__ __launch_bounds__(BLK) void k_closed_loop(gym_model mm, gym_weights w, const double2* __restrict__ x,
-                                                     const double2* __restrict__ u, const double2* __restrict__ Kf,
-                                                     const double2* __restrict__ s, const double* __restrict__ gamma,
+                                                     const double* __restrict__ u, const double2* __restrict__ Kf,
+                                                     const double* __restrict__ s, const double* __restrict__ gamma,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
-                                                     double2* __restrict__ xn, double2* __restrict__ un,
+                                                     double2* __restrict__ xn, double* __restrict__ un,
                                                      double* __restrict__ cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
     const Dyn m(mm);
     const double2 a = x[l], b = x[Bp + l];
-    const double J =
-        rollout<K_FULL, true>(m, w, x, u, Kf, s, xr, ur, xn, un, gamma[l], l, Bp, N, a.x, a.y, b.x, b.y);
+    const double J = rollout_ref<true>(m, w, x, u, Kf, s, xr, ur, xn, un, gamma[l], l, Bp, N, a.x, a.y, b.x, b.y);
     if (cost) cost[l] = J;
 }
 
@@ -303,45 +362,8 @@ __global__ void k_point(gym_model mm, const double* __restrict__ x, const double
 struct Mat4 { double v[16]; };
 struct Mat2 { double v[4]; };
 
-__global__ void k_stage_cost_derivs(const double* __restrict__ x, const double* __restrict__ xr,
-                                    const double* __restrict__ u, const double* __restrict__ ur, Mat4 Q, Mat2 R,
-                                    int terminal, double* __restrict__ lo, double* __restrict__ gx,
-                                    double* __restrict__ gu, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    double e[4], Qe[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = x[4 * i + k] - xr[4 * i + k];
-    double l = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s += Q.v[4 * r + k] * e[k];
-        Qe[r] = s;
-    }
-    // e^T Q e evaluated as (e^T Q) e
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s += e[k] * Q.v[4 * k + c];
-        l += s * e[c];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gx[4 * i + r] = 2.0 * Qe[r];
-    if (!terminal) {
-        const double f0 = u[2 * i] - ur[2 * i], f1 = u[2 * i + 1] - ur[2 * i + 1];
-        const double lu = (f0 * R.v[0] + f1 * R.v[2]) * f0 + (f0 * R.v[1] + f1 * R.v[3]) * f1;
-        l += lu;
-        gu[2 * i] = 2.0 * (R.v[0] * f0 + R.v[1] * f1);
-        gu[2 * i + 1] = 2.0 * (R.v[2] * f0 + R.v[3] * f1);
-    }
-    lo[i] = l;
-}
-
 __device__ __forceinline__ double quad4(const double* M, const double e[4]) {
-    double l = 0.0;
+    double l = 0.0;  // (e^T M) e
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         double s = 0.0;
@@ -352,7 +374,37 @@ __device__ __forceinline__ double quad4(const double* M, const double e[4]) {
     return l;
 }
 
-__global__ __launch_bounds__(BLK) void k_total_cost(const double2* __restrict__ x, const double2* __restrict__ u,
+__device__ __forceinline__ double quad2(const double* M, double f0, double f1) {
+    return (f0 * M[0] + f1 * M[2]) * f0 + (f0 * M[1] + f1 * M[3]) * f1;
+}
+
+__global__ void k_stage_cost_derivs(const double* __restrict__ x, const double* __restrict__ xr,
+                                    const double* __restrict__ u, const double* __restrict__ ur, Mat4 Q, Mat2 R,
+                                    int terminal, double* __restrict__ lo, double* __restrict__ gx,
+                                    double* __restrict__ gu, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = x[4 * i + k] - xr[4 * i + k];
+    double l = quad4(Q.v, e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += Q.v[4 * r + k] * e[k];
+        gx[4 * i + r] = 2.0 * s;
+    }
+    if (!terminal) {
+        const double f0 = u[2 * i] - ur[2 * i], f1 = u[2 * i + 1] - ur[2 * i + 1];
+        l += quad2(R.v, f0, f1);
+        gu[2 * i] = 2.0 * (R.v[0] * f0 + R.v[1] * f1);
+        gu[2 * i + 1] = 2.0 * (R.v[2] * f0 + R.v[3] * f1);
+    }
+    lo[i] = l;
+}
+
+__global__ __launch_bounds__(BLK) void k_total_cost(const double2* __restrict__ x, const double* __restrict__ u,
                                                     const double* __restrict__ xr, const double* __restrict__ ur,
                                                     Mat4 Q, Mat2 R, Mat4 QT, double* __restrict__ cost, int64_t B,
                                                     int64_t Bp, int N) {
@@ -360,22 +412,20 @@ __global__ __launch_bounds__(BLK) void k_total_cost(const double2* __restrict__ 
     if (l >= B) return;
     double J = 0.0;
     for (int t = 0; t < N - 1; ++t) {
-        const double2 a = x[((int64_t)t * 2) * Bp + l], b = x[((int64_t)t * 2 + 1) * Bp + l];
-        const double2 v = u[(int64_t)t * Bp + l];
+        const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
         const double e[4] = {a.x - xr[4 * t], a.y - xr[4 * t + 1], b.x - xr[4 * t + 2], b.y - xr[4 * t + 3]};
         J += quad4(Q.v, e);
-        const double f0 = v.x - ur[2 * t], f1 = v.y - ur[2 * t + 1];
-        J += (f0 * R.v[0] + f1 * R.v[2]) * f0 + (f0 * R.v[1] + f1 * R.v[3]) * f1;
+        J += quad2(R.v, u[pix(t, 0, 2, l, Bp)] - ur[2 * t], u[pix(t, 1, 2, l, Bp)] - ur[2 * t + 1]);
     }
     const int T = N - 1;
-    const double2 a = x[((int64_t)T * 2) * Bp + l], b = x[((int64_t)T * 2 + 1) * Bp + l];
+    const double2 a = x[pix(T, 0, 2, l, Bp)], b = x[pix(T, 1, 2, l, Bp)];
     const double e[4] = {a.x - xr[4 * T], a.y - xr[4 * T + 1], b.x - xr[4 * T + 2], b.y - xr[4 * T + 3]};
     cost[l] = J + quad4(QT.v, e);
 }
 
 // build_stage_lists (:166-181) as plain-double SoA for the generic Riccati path
 __global__ __launch_bounds__(BLK) void k_linearize(gym_model mm, gym_weights w, const double2* __restrict__ x,
-                                                   const double2* __restrict__ u, const double* __restrict__ xr,
+                                                   const double* __restrict__ u, const double* __restrict__ xr,
                                                    const double* __restrict__ ur, double* __restrict__ Ad,
                                                    double* __restrict__ Bd, double* __restrict__ q,
                                                    double* __restrict__ r, double* __restrict__ qT, int64_t B,
@@ -386,9 +436,9 @@ __global__ __launch_bounds__(BLK) void k_linearize(gym_model mm, gym_weights w, 
     const double dt = m.h;
     const int T = N - 1;
     for (int t = 0; t < T; ++t) {
-        const double2 a = x[((int64_t)t * 2) * Bp + l], b = x[((int64_t)t * 2 + 1) * Bp + l];
-        const double2 v = u[(int64_t)t * Bp + l];
-        const gym::Jac J = gym::jacobian(m, a.x, a.y, b.x, b.y, v.y);
+        const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
+        const double v0 = u[pix(t, 0, 2, l, Bp)], v1 = u[pix(t, 1, 2, l, Bp)];
+        const gym::Jac J = gym::jacobian(m, a.x, a.y, b.x, b.y, v1);
         double A[16] = {1.0, 0.0, dt, 0.0, 0.0, 1.0, 0.0, dt};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -403,10 +453,10 @@ __global__ __launch_bounds__(BLK) void k_linearize(gym_model mm, gym_weights w, 
         const double xe[4] = {a.x - xr[4 * t], a.y - xr[4 * t + 1], b.x - xr[4 * t + 2], b.y - xr[4 * t + 3]};
 #pragma unroll
         for (int c = 0; c < 4; ++c) q[((int64_t)t * 4 + c) * Bp + l] = (2.0 * w.Q[c]) * xe[c];
-        r[((int64_t)t * 2) * Bp + l] = (2.0 * w.R[0]) * (v.x - ur[2 * t]);
-        r[((int64_t)t * 2 + 1) * Bp + l] = (2.0 * w.R[1]) * (v.y - ur[2 * t + 1]);
+        r[((int64_t)t * 2) * Bp + l] = (2.0 * w.R[0]) * (v0 - ur[2 * t]);
+        r[((int64_t)t * 2 + 1) * Bp + l] = (2.0 * w.R[1]) * (v1 - ur[2 * t + 1]);
     }
-    const double2 a = x[((int64_t)T * 2) * Bp + l], b = x[((int64_t)T * 2 + 1) * Bp + l];
+    const double2 a = x[pix(T, 0, 2, l, Bp)], b = x[pix(T, 1, 2, l, Bp)];
     const double xe[4] = {a.x - xr[4 * T], a.y - xr[4 * T + 1], b.x - xr[4 * T + 2], b.y - xr[4 * T + 3]};
 #pragma unroll
     for (int c = 0; c < 4; ++c) qT[(int64_t)c * Bp + l] = (2.0 * w.QT[c]) * xe[c];
@@ -453,7 +503,6 @@ __global__ __launch_bounds__(BLK) void k_riccati_general(
         for (int c = 0; c < 16; ++c) a[c] = A[((int64_t)t * 16 + c) * Bp + l];
 #pragma unroll
         for (int c = 0; c < 8; ++c) b[c] = Bm[((int64_t)t * 8 + c) * Bp + l];
-        // PB (4x2), PA (4x4)
         double PB[8], PA[16];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -504,7 +553,6 @@ __global__ __launch_bounds__(BLK) void k_riccati_general(
             st[i] = -Y[i][4];
         }
         dJ += g0 * st[0] + g1 * st[1];
-        // GK (2x4), Gs (2)
         double GK[8], Gs[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -540,39 +588,34 @@ __global__ __launch_bounds__(BLK) void k_riccati_general(
 }
 
 // ------------------------------------------------------------------------------------------
-// kernels: layout
+// kernels: layout.  Lane-major (B, L, C) <-> SoA (L, C/W, Bp, W), W = 1 (planes) or 2 (pairs).
 // ------------------------------------------------------------------------------------------
-__global__ void k_pack(const double* __restrict__ src, double2* __restrict__ dst, int64_t B, int64_t Bp, int L,
-                       int C) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int P = C / 2;
+__global__ void k_pack(const double* __restrict__ src, double* __restrict__ dst, int64_t B, int64_t Bp, int L,
+                       int C, int W) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // element (of W doubles) index
+    const int P = C / W;
     if (i >= (int64_t)L * P * Bp) return;
     const int64_t lane = i % Bp;
     const int64_t rest = i / Bp;
     const int p = (int)(rest % P);
     const int64_t t = rest / P;
-    double2 v = make_double2(0.0, 0.0);
-    if (lane < B) {
-        const double* s = src + (lane * L + t) * C + 2 * p;
-        v = make_double2(s[0], s[1]);
-    }
-    dst[i] = v;
+    const double* s = src + (lane * L + t) * C + W * p;
+    for (int k = 0; k < W; ++k) dst[W * i + k] = (lane < B) ? s[k] : 0.0;
 }
 
-__global__ void k_unpack(const double2* __restrict__ s0, const double2* __restrict__ s1,
+__global__ void k_unpack(const double* __restrict__ s0, const double* __restrict__ s1,
                          const int32_t* __restrict__ sel, double* __restrict__ dst, int64_t B, int64_t Bp, int L,
-                         int C) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // output pair index, lane-major
-    const int P = C / 2;
+                         int C, int W) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // output element index, lane-major
+    const int P = C / W;
     if (o >= B * L * P) return;
     const int p = (int)(o % P);
     const int64_t rest = o / P;
     const int64_t t = rest % L;
     const int64_t lane = rest / L;
-    const double2* s = (sel && sel[lane]) ? s1 : s0;
-    const double2 v = s[(t * P + p) * Bp + lane];
-    dst[2 * o] = v.x;
-    dst[2 * o + 1] = v.y;
+    const double* s = (sel && sel[lane]) ? s1 : s0;
+    const double* e = s + W * ((t * P + p) * Bp + lane);
+    for (int k = 0; k < W; ++k) dst[W * o + k] = e[k];
 }
 
 __global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restrict__ K, int64_t B, int64_t Bp,
@@ -580,7 +623,7 @@ __global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restric
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (lane, t)
     if (o >= B * T) return;
     const int64_t t = o % T, lane = o / T;
-    const double2 a = K1[(t * 2) * Bp + lane], b = K1[(t * 2 + 1) * Bp + lane];
+    const double2 a = K1[pix((int)t, 0, 2, lane, Bp)], b = K1[pix((int)t, 1, 2, lane, Bp)];
     double* d = K + 8 * o;
     d[0] = 0.0; d[1] = 0.0; d[2] = 0.0; d[3] = 0.0;
     d[4] = a.x; d[5] = a.y; d[6] = b.x; d[7] = b.y;
@@ -590,7 +633,7 @@ __global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restric
 // kernels: batched Newton / Armijo solver (newton_Algorithm :298-398)
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const double* __restrict__ x0,
-                                              const double2* __restrict__ u, const double* __restrict__ xr,
+                                              const double* __restrict__ u, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ xn,
                                               double* __restrict__ cost, int32_t* __restrict__ status,
                                               int32_t* __restrict__ n_iter, int32_t* __restrict__ res_buf,
@@ -607,22 +650,23 @@ __global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const
     }
     status[l] = GYM_ACTIVE;
     const Dyn m(mm);
-    cost[l] = rollout<K_OPEN, true>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
-                                    x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
+    cost[l] = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
+                                 x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
 }
 
-__global__ __launch_bounds__(BLK) void k_nt_backward(gym_model mm, gym_weights w, const double2* __restrict__ x,
-                                                     const double2* __restrict__ u, const double* __restrict__ xr,
-                                                     const double* __restrict__ ur, double2* __restrict__ K1,
-                                                     double2* __restrict__ sig, double* __restrict__ dJ,
-                                                     double* __restrict__ smax, const int32_t* __restrict__ status,
-                                                     double* __restrict__ hist_smax, int64_t B, int64_t Bp, int N,
-                                                     int k, int hist_len) {
+__global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weights w, const double2* __restrict__ x,
+                                                        const double* __restrict__ u, const double* __restrict__ xr,
+                                                        const double* __restrict__ ur, double2* __restrict__ K1,
+                                                        double2* __restrict__ cs, double* __restrict__ dJ,
+                                                        double* __restrict__ smax,
+                                                        const int32_t* __restrict__ status,
+                                                        double* __restrict__ hist_smax, int64_t B, int64_t Bp, int N,
+                                                        int k, int hist_len) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B || status[l] != GYM_ACTIVE) return;
     const Dyn m(mm);
     double d, s;
-    backward_lane<false>(m, w, x, u, xr, ur, K1, sig, nullptr, l, Bp, N, d, s);
+    backward_lane<true, false>(m, w, x, u, xr, ur, K1, cs, nullptr, nullptr, l, Bp, N, d, s);
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
@@ -651,23 +695,23 @@ __device__ __forceinline__ void fail_lane(const SolverCtl& a, int64_t l, int32_t
 }
 
 // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost.
-__global__ __launch_bounds__(BLK) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a,
-                                                  const double2* __restrict__ x, const double2* __restrict__ u,
-                                                  const double2* __restrict__ K1, const double2* __restrict__ sig,
-                                                  const double* __restrict__ xr, const double* __restrict__ ur,
-                                                  double2* __restrict__ xn, double2* __restrict__ un,
-                                                  double* __restrict__ cost, const double* __restrict__ dJ,
-                                                  const double* __restrict__ smax, double* __restrict__ gamma,
-                                                  int32_t* __restrict__ status, int32_t* __restrict__ n_iter,
-                                                  int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
-                                                  int32_t* __restrict__ retry_list, int32_t* __restrict__ counters,
-                                                  double* __restrict__ hist_cost, int64_t B, int64_t Bp, int N) {
+__global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a,
+                                                     const double2* __restrict__ x, const double* __restrict__ u,
+                                                     const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                     const double* __restrict__ xr, const double* __restrict__ ur,
+                                                     double2* __restrict__ xn, double* __restrict__ un,
+                                                     double* __restrict__ cost, const double* __restrict__ dJ,
+                                                     const double* __restrict__ smax, double* __restrict__ gamma,
+                                                     int32_t* __restrict__ status, int32_t* __restrict__ n_iter,
+                                                     int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
+                                                     int32_t* __restrict__ retry_list, int32_t* __restrict__ counters,
+                                                     double* __restrict__ hist_cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B || status[l] != GYM_ACTIVE) return;
     const Dyn m(mm);
     const double2 xa = x[l], xb = x[Bp + l];
     const double g = a.gamma0;
-    const double Jn = rollout<K_COMPACT, true>(m, w, x, u, K1, sig, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+    const double Jn = rollout_cform<true>(m, w, u, K1, cs, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
     n_roll[l] += 1;
     if (Jn < cost[l] + a.c * g * dJ[l]) {  // strict Armijo test (:361)
         n_iter[l] += 1;
@@ -683,11 +727,10 @@ __global__ __launch_bounds__(BLK) void k_nt_trial(gym_model mm, gym_weights w, S
 
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
 __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights w, SolverCtl a,
-                                                       const double2* __restrict__ x, const double2* __restrict__ u,
-                                                       const double2* __restrict__ K1,
-                                                       const double2* __restrict__ sig, const double* __restrict__ xr,
-                                                       const double* __restrict__ ur, const double* __restrict__ cost,
-                                                       const double* __restrict__ dJ,
+                                                       const double2* __restrict__ x, const double* __restrict__ u,
+                                                       const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                       const double* __restrict__ xr, const double* __restrict__ ur,
+                                                       const double* __restrict__ cost, const double* __restrict__ dJ,
                                                        const int32_t* __restrict__ retry_list,
                                                        const int32_t* __restrict__ counters,
                                                        uint8_t* __restrict__ cand_ok, int64_t Bp, int N) {
@@ -701,18 +744,18 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
         const double2 xa = x[l], xb = x[Bp + l];
-        const double Jn = rollout<K_COMPACT, false>(m, w, x, u, K1, sig, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x,
-                                                    xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<false>(m, w, u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x, xa.y,
+                                               xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
     }
 }
 
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
 __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, SolverCtl a,
-                                                  const double2* __restrict__ x, const double2* __restrict__ u,
-                                                  const double2* __restrict__ K1, const double2* __restrict__ sig,
+                                                  const double2* __restrict__ x, const double* __restrict__ u,
+                                                  const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
-                                                  double2* __restrict__ xn, double2* __restrict__ un,
+                                                  double2* __restrict__ xn, double* __restrict__ un,
                                                   double* __restrict__ cost, const double* __restrict__ smax,
                                                   double* __restrict__ gamma, int32_t* __restrict__ status,
                                                   int32_t* __restrict__ n_iter, int32_t* __restrict__ res_buf,
@@ -738,8 +781,7 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, S
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
         const double2 xa = x[l], xb = x[Bp + l];
-        const double Jn =
-            rollout<K_COMPACT, true>(m, w, x, u, K1, sig, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<true>(m, w, u, K1, cs, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -807,6 +849,28 @@ __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restr
         status[l] = GYM_MAX_ITERS;
         res_buf[l] = k_done & 1;
     }
+}
+
+// sigma of each lane's last iteration, lane-major (B,T,2): sigma1 from the sweep's (c1, sigma1) stream,
+// sigma0 = -(2R0 (u0 - ur0)) / (2R0) recomputed from that iteration's controls, buffer (n_iter-1) & 1.
+__global__ void k_finalize_sigma(gym_weights w, const double2* __restrict__ cs, const double* __restrict__ u0b,
+                                 const double* __restrict__ u1b, const double* __restrict__ ur,
+                                 const int32_t* __restrict__ n_iter, double* __restrict__ sig, int64_t B, int64_t Bp,
+                                 int T) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (lane, t)
+    if (o >= B * T) return;
+    const int t = (int)(o % T);
+    const int64_t lane = o / T;
+    const int it = n_iter[lane];
+    double s0 = 0.0, s1 = 0.0;
+    if (it > 0) {
+        const double* u = ((it - 1) & 1) ? u1b : u0b;
+        const double G00 = 2.0 * w.R[0];
+        s0 = -(G00 * (u[pix(t, 0, 2, lane, Bp)] - ur[2 * t])) * (1.0 / G00);
+        s1 = cs[(int64_t)t * Bp + lane].y;
+    }
+    sig[2 * o] = s0;
+    sig[2 * o + 1] = s1;
 }
 
 struct TimedLaunch {  // records a start/stop event pair around one launch if the slot is free
@@ -886,19 +950,20 @@ int gym_stage_cost_derivs(const double* x, const double* xr, const double* u, co
     return launch_status();
 }
 
-int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, void* s) {
-    if (!src || !dst || bad_dims(B, Bp, 2) || L <= 0 || C <= 0 || (C % 2)) return GYM_EINVAL;
-    const int64_t n = (int64_t)L * (C / 2) * Bp;
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, src, (double2*)dst, B, Bp, L, C);
+int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, int32_t W, void* s) {
+    if (!src || !dst || bad_dims(B, Bp, 2) || L <= 0 || C <= 0 || (W != 1 && W != 2) || (C % W)) return GYM_EINVAL;
+    const int64_t n = (int64_t)L * (C / W) * Bp;
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, src, dst, B, Bp, L, C, W);
     return launch_status();
 }
 
 int gym_unpack_lanes(const double* s0, const double* s1, const int32_t* sel, double* dst, int64_t B, int64_t Bp,
-                     int32_t L, int32_t C, void* s) {
-    if (!s0 || !dst || bad_dims(B, Bp, 2) || L <= 0 || C <= 0 || (C % 2) || (sel && !s1)) return GYM_EINVAL;
-    const int64_t n = B * L * (C / 2);
-    hipLaunchKernelGGL(k_unpack, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, (const double2*)s0,
-                       (const double2*)(s1 ? s1 : s0), sel, dst, B, Bp, L, C);
+                     int32_t L, int32_t C, int32_t W, void* s) {
+    if (!s0 || !dst || bad_dims(B, Bp, 2) || L <= 0 || C <= 0 || (W != 1 && W != 2) || (C % W) || (sel && !s1))
+        return GYM_EINVAL;
+    const int64_t n = B * L * (C / W);
+    hipLaunchKernelGGL(k_unpack, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, s0, s1 ? s1 : s0, sel, dst, B,
+                       Bp, L, C, W);
     return launch_status();
 }
 
@@ -913,8 +978,8 @@ int gym_rollout_open_loop(const gym_model* m, const gym_weights* w, const double
                           const double* xr, const double* ur, double* x, double* cost, int64_t B, int64_t Bp,
                           int32_t N, void* s) {
     if (!m || !w || !x0 || !u || !xr || !ur || !x || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_open_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, x0,
-                       (const double2*)u, xr, ur, (double2*)x, cost, B, Bp, N);
+    hipLaunchKernelGGL(k_open_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, x0, u, xr, ur,
+                       (double2*)x, cost, B, Bp, N);
     return launch_status();
 }
 
@@ -924,16 +989,16 @@ int gym_closed_loop(const gym_model* m, const gym_weights* w, const double* x, c
     if (!m || !w || !x || !u || !Kf || !sigma || !gamma || !xr || !ur || !xn || !un || bad_dims(B, Bp, N))
         return GYM_EINVAL;
     hipLaunchKernelGGL(k_closed_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w,
-                       (const double2*)x, (const double2*)u, (const double2*)Kf, (const double2*)sigma, gamma, xr, ur,
-                       (double2*)xn, (double2*)un, cost, B, Bp, N);
+                       (const double2*)x, u, (const double2*)Kf, sigma, gamma, xr, ur, (double2*)xn, un, cost, B, Bp,
+                       N);
     return launch_status();
 }
 
 int gym_total_cost(const double* x, const double* u, const double* xr, const double* ur, const double Q[16],
                    const double R[4], const double QT[16], double* cost, int64_t B, int64_t Bp, int32_t N, void* s) {
     if (!x || !u || !xr || !ur || !Q || !R || !QT || !cost || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_total_cost, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, (const double2*)x,
-                       (const double2*)u, xr, ur, mat4(Q), mat2(R), mat4(QT), cost, B, Bp, N);
+    hipLaunchKernelGGL(k_total_cost, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, (const double2*)x, u, xr,
+                       ur, mat4(Q), mat2(R), mat4(QT), cost, B, Bp, N);
     return launch_status();
 }
 
@@ -942,8 +1007,7 @@ int gym_backward_sweep(const gym_model* m, const gym_weights* w, const double* x
                        int64_t Bp, int32_t N, void* s) {
     if (!m || !w || !x || !u || !xr || !ur || !K1 || !sigma || bad_dims(B, Bp, N)) return GYM_EINVAL;
     hipLaunchKernelGGL(k_backward_api, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w,
-                       (const double2*)x, (const double2*)u, xr, ur, (double2*)K1, (double2*)sigma, dJ, smax,
-                       (double2*)lambda, B, Bp, N);
+                       (const double2*)x, u, xr, ur, (double2*)K1, sigma, dJ, smax, (double2*)lambda, B, Bp, N);
     return launch_status();
 }
 
@@ -951,8 +1015,8 @@ int gym_linearize(const gym_model* m, const gym_weights* w, const double* x, con
                   const double* ur, double* Ad, double* Bd, double* q, double* r, double* qT, int64_t B, int64_t Bp,
                   int32_t N, void* s) {
     if (!m || !w || !x || !u || !xr || !ur || !Ad || !Bd || !q || !r || !qT || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_linearize, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, (const double2*)x,
-                       (const double2*)u, xr, ur, Ad, Bd, q, r, qT, B, Bp, N);
+    hipLaunchKernelGGL(k_linearize, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, (const double2*)x, u,
+                       xr, ur, Ad, Bd, q, r, qT, B, Bp, N);
     return launch_status();
 }
 
@@ -967,9 +1031,9 @@ int gym_riccati_general(const double* A, const double* Bm, const double* Q, cons
 }
 
 static bool bad_batch(const gym_batch* b) {
-    return !b || bad_dims(b->B, b->Bp, b->N) || !b->x[0] || !b->x[1] || !b->u[0] || !b->u[1] || !b->K1 ||
-           !b->sigma || !b->x_ref || !b->u_ref || !b->cost || !b->dJ || !b->smax || !b->gamma || !b->status ||
-           !b->n_iter || !b->res_buf || !b->n_roll || !b->retry_list || !b->counters || !b->partials || !b->stats;
+    return !b || bad_dims(b->B, b->Bp, b->N) || !b->x[0] || !b->x[1] || !b->u[0] || !b->u[1] || !b->K1 || !b->cs ||
+           !b->x_ref || !b->u_ref || !b->cost || !b->dJ || !b->smax || !b->gamma || !b->status || !b->n_iter ||
+           !b->res_buf || !b->n_roll || !b->retry_list || !b->counters || !b->partials || !b->stats;
 }
 
 int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, const gym_batch* b, void* s) {
@@ -980,9 +1044,9 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(b->counters, 0, sizeof(int32_t) * 4, st);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, *m, *w, x0, (const double2*)b->u[0],
-                       b->x_ref, b->u_ref, (double2*)b->x[0], b->cost, b->status, b->n_iter, b->res_buf, b->n_roll,
-                       b->gamma, b->smax, b->dJ, b->B, b->Bp, b->N);
+    hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, *m, *w, x0, b->u[0], b->x_ref, b->u_ref,
+                       (double2*)b->x[0], b->cost, b->status, b->n_iter, b->res_buf, b->n_roll, b->gamma, b->smax,
+                       b->dJ, b->B, b->Bp, b->N);
     return launch_status();
 }
 
@@ -992,39 +1056,38 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     hipStream_t st = (hipStream_t)s;
     const int cur = k & 1, nxt = (k + 1) & 1;
     const double2* x = (const double2*)b->x[cur];
-    const double2* u = (const double2*)b->u[cur];
+    const double* u = b->u[cur];
     double2* xn = (double2*)b->x[nxt];
-    double2* un = (double2*)b->u[nxt];
+    double* un = b->u[nxt];
+    const double2* K1 = (const double2*)b->K1;
+    const double2* cs = (const double2*)b->cs;
     const int grid = grid_for(b->B, BLK);
     const bool hist = a->record_history != 0;
     {
-    TimedLaunch tl(b->timing, 0, st);
-    hipLaunchKernelGGL(k_nt_backward, dim3(grid), dim3(BLK), 0, st, *m, *w, x, u, b->x_ref, b->u_ref,
-                       (double2*)b->K1, (double2*)b->sigma, b->dJ, b->smax, b->status,
-                       hist ? b->hist_smax : nullptr, b->B, b->Bp, b->N, k, b->hist_len);
+        TimedLaunch tl(b->timing, 0, st);
+        hipLaunchKernelGGL(k_nt_backward, dim3(grid), dim3(BLK), 0, st, *m, *w, x, u, b->x_ref, b->u_ref,
+                           (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
+                           hist ? b->hist_smax : nullptr, b->B, b->Bp, b->N, k, b->hist_len);
     }
     SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     double* hc = hist ? b->hist_cost : nullptr;
     {
-    TimedLaunch tl(b->timing, 1, st);
-    hipLaunchKernelGGL(k_nt_trial, dim3(grid), dim3(BLK), 0, st, *m, *w, c, x, u, (const double2*)b->K1,
-                       (const double2*)b->sigma, b->x_ref, b->u_ref, xn, un, b->cost, b->dJ, b->smax, b->gamma,
-                       b->status, b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hc, b->B, b->Bp,
-                       b->N);
+        TimedLaunch tl(b->timing, 1, st);
+        hipLaunchKernelGGL(k_nt_trial, dim3(grid), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs, b->x_ref, b->u_ref, xn,
+                           un, b->cost, b->dJ, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
+                           b->retry_list, b->counters, hc, b->B, b->Bp, b->N);
     }
     if (a->max_ls > 1) {
-        const int gc = grid_for(b->B * (int64_t)(a->max_ls - 1), BLK, 4096);
         {
-        TimedLaunch tl(b->timing, 2, st);
-        hipLaunchKernelGGL(k_nt_candidates, dim3(gc), dim3(BLK), 0, st, *m, *w, c, x, u, (const double2*)b->K1,
-                           (const double2*)b->sigma, b->x_ref, b->u_ref, b->cost, b->dJ, b->retry_list, b->counters,
-                           b->cand_ok, b->Bp, b->N);
+            TimedLaunch tl(b->timing, 2, st);
+            const int gc = grid_for(b->B * (int64_t)(a->max_ls - 1), BLK, 4096);
+            hipLaunchKernelGGL(k_nt_candidates, dim3(gc), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs, b->x_ref,
+                               b->u_ref, b->cost, b->dJ, b->retry_list, b->counters, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(k_nt_retry, dim3(grid_for(b->B, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, x, u,
-                           (const double2*)b->K1, (const double2*)b->sigma, b->x_ref, b->u_ref, xn, un, b->cost,
-                           b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters,
-                           b->cand_ok, hc, b->Bp, b->N);
+        hipLaunchKernelGGL(k_nt_retry, dim3(grid_for(b->B, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs,
+                           b->x_ref, b->u_ref, xn, un, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf,
+                           b->n_roll, b->retry_list, b->counters, b->cand_ok, hc, b->Bp, b->N);
     }
     TimedLaunch tl(b->timing, 4, st);
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
@@ -1033,20 +1096,28 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     return launch_status();
 }
 
-int gym_newton_finalize(const gym_batch* b, int32_t k_done, double* x_out, double* u_out, double* K_out,
-                        double* sig_out, void* s) {
-    if (bad_batch(b) || k_done < 0) return GYM_EINVAL;
+int gym_newton_finalize(const gym_weights* w, const gym_batch* b, int32_t k_done, double* x_out, double* u_out,
+                        double* K_out, double* sig_out, void* s) {
+    if (!w || bad_batch(b) || k_done < 0) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     hipLaunchKernelGGL(k_finalize_status, dim3(grid_for(b->B, 256)), dim3(256), 0, st, b->status, b->res_buf, b->B,
                        (int)k_done);
     int e = launch_status();
     if (e) return e;
     const int T = b->N - 1;
-    if (x_out && (e = gym_unpack_lanes(b->x[0], b->x[1], b->res_buf, x_out, b->B, b->Bp, b->N, 4, s))) return e;
-    if (u_out && (e = gym_unpack_lanes(b->u[0], b->u[1], b->res_buf, u_out, b->B, b->Bp, T, 2, s))) return e;
+    if (x_out && (e = gym_unpack_lanes(b->x[0], b->x[1], b->res_buf, x_out, b->B, b->Bp, b->N, 4, 2, s))) return e;
+    if (u_out && (e = gym_unpack_lanes(b->u[0], b->u[1], b->res_buf, u_out, b->B, b->Bp, T, 2, 1, s))) return e;
     if (K_out && (e = gym_unpack_gains(b->K1, K_out, b->B, b->Bp, T, s))) return e;
-    if (sig_out && (e = gym_unpack_lanes(b->sigma, nullptr, nullptr, sig_out, b->B, b->Bp, T, 2, s))) return e;
+    if (sig_out && (e = gym_newton_sigma(w, b, sig_out, s))) return e;
     return 0;
+}
+
+int gym_newton_sigma(const gym_weights* w, const gym_batch* b, double* sig_out, void* s) {
+    if (!w || bad_batch(b) || !sig_out) return GYM_EINVAL;
+    const int T = b->N - 1;
+    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, (hipStream_t)s, *w,
+                       (const double2*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
+    return launch_status();
 }
 
 int gym_timing_create(gym_timing* t) {

@@ -55,9 +55,10 @@ class Weights:
 class AcrobotEngine:
     """Launchers for one acrobot parameter set on one HIP device."""
 
-    def __init__(self, params=1, dt: float = DT, weights: Weights | None = None, device=None):
-        self.device = _lib.require_device(device)
-        self.lib = _lib.load()
+    def __init__(self, params=1, dt: float = DT, weights: Weights | None = None, device=None,
+                 lib_path: str = _lib.LIB_PATH):
+        self.device = _lib.require_device(device, lib_path)
+        self.lib = _lib.load(lib_path)
         p = PARAM_SETS[params] if isinstance(params, int) else params
         self.params = dict(p)
         self.dt = float(dt)
@@ -87,20 +88,21 @@ class AcrobotEngine:
         self.weights = weights
         self._w = weights.c_struct()
 
-    def pack(self, a: torch.Tensor, Bp: int) -> torch.Tensor:
-        """(B,L,C) lane-major -> SoA (L, C/2, Bp, 2)."""
+    def pack(self, a: torch.Tensor, Bp: int, W: int = 2) -> torch.Tensor:
+        """(B,L,C) lane-major -> SoA (L, C/W, Bp, W): W = 2 pairs (states, gains), W = 1 planes (controls, sigma)."""
         B, L, Cc = a.shape
-        out = torch.empty((L, Cc // 2, Bp, 2), dtype=F64, device=self.device)
-        _lib.check(self.lib.gym_pack_lanes(a.data_ptr(), out.data_ptr(), B, Bp, L, Cc, self.stream),
+        out = torch.empty((L, Cc // W, Bp, W), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_pack_lanes(a.data_ptr(), out.data_ptr(), B, Bp, L, Cc, W, self.stream),
                    "gym_pack_lanes")
         return out
 
     def unpack(self, soa: torch.Tensor, B: int, soa1: torch.Tensor | None = None,
                sel: torch.Tensor | None = None) -> torch.Tensor:
-        L, P, Bp, _ = soa.shape
-        out = torch.empty((B, L, 2 * P), dtype=F64, device=self.device)
+        """SoA (L, P, Bp, W) -> lane-major (B, L, P*W); lane b reads soa1 where sel[b] != 0."""
+        L, P, Bp, W = soa.shape
+        out = torch.empty((B, L, P * W), dtype=F64, device=self.device)
         _lib.check(self.lib.gym_unpack_lanes(soa.data_ptr(), _lib.ptr(soa1), _lib.ptr(sel), out.data_ptr(), B, Bp,
-                                             L, 2 * P, self.stream), "gym_unpack_lanes")
+                                             L, P * W, W, self.stream), "gym_unpack_lanes")
         return out
 
     def refs(self, x_ref, u_ref):
@@ -175,7 +177,7 @@ class AcrobotEngine:
         if u.shape != (B, N - 1, 2):
             raise ValueError(f"u must be ({B},{N - 1},2), got {tuple(u.shape)}")
         Bp = padded(B)
-        us = self.pack(u, Bp)
+        us = self.pack(u, Bp, W=1)
         xs = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device)
         J = torch.empty(Bp, dtype=F64, device=self.device)
         _lib.check(self.lib.gym_rollout_open_loop(C.byref(self.model), C.byref(self._w), x0.data_ptr(),
@@ -192,9 +194,9 @@ class AcrobotEngine:
         Bp = padded(B)
         g = torch.zeros(Bp, dtype=F64, device=self.device)
         g[:B] = self.t(gamma).reshape(-1).expand(B) if self.t(gamma).numel() == 1 else self.t(gamma).reshape(B)
-        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp, W=1)
         Ks = self.pack(K.reshape(B, T, 8), Bp)
-        ss = self.pack(sigma, Bp)
+        ss = self.pack(sigma, Bp, W=1)
         xn = torch.empty_like(xs); un = torch.empty_like(us)
         J = torch.empty(Bp, dtype=F64, device=self.device)
         _lib.check(self.lib.gym_closed_loop(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),
@@ -208,7 +210,7 @@ class AcrobotEngine:
         B, N, _ = x.shape
         x_ref = self.t(x_ref); u_ref = self.t(u_ref)[: N - 1].contiguous()
         Bp = padded(B)
-        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp, W=1)
         mats = [np.ascontiguousarray(np.asarray(M, float)) for M in (Q, R, QT)]
         J = torch.empty(Bp, dtype=F64, device=self.device)
         _lib.check(self.lib.gym_total_cost(xs.data_ptr(), us.data_ptr(), x_ref.data_ptr(), u_ref.data_ptr(),
@@ -223,9 +225,9 @@ class AcrobotEngine:
         T = N - 1
         x_ref, u_ref = self.refs(x_ref, u_ref)
         Bp = padded(B)
-        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp, W=1)
         K1 = torch.empty((T, 2, Bp, 2), dtype=F64, device=self.device)
-        sg = torch.empty((T, 1, Bp, 2), dtype=F64, device=self.device)
+        sg = torch.empty((T, 2, Bp, 1), dtype=F64, device=self.device)
         dJ = torch.empty(Bp, dtype=F64, device=self.device)
         sm = torch.empty(Bp, dtype=F64, device=self.device)
         lam = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device) if want_lambda else None
@@ -244,7 +246,7 @@ class AcrobotEngine:
         T = N - 1
         x_ref, u_ref = self.refs(x_ref, u_ref)
         Bp = padded(B)
-        xs, us = self.pack(x, Bp), self.pack(u, Bp)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp, W=1)
         e = lambda *s: torch.empty(s, dtype=F64, device=self.device)  # noqa: E731
         Ad, Bd, q, r, qT = e(T, 16, Bp), e(T, 8, Bp), e(T, 4, Bp), e(T, 2, Bp), e(4, Bp)
         _lib.check(self.lib.gym_linearize(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),

@@ -69,9 +69,9 @@ class BatchedNewtonSolver:
         e = lambda *s, dt=F64: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
         Bp, N, T = self.Bp, self.N, self.T
         self.x = [e(N, 2, Bp, 2), e(N, 2, Bp, 2)]
-        self.u = [e(T, 1, Bp, 2), e(T, 1, Bp, 2)]
-        self.K1 = e(T, 2, Bp, 2)
-        self.sigma = e(T, 1, Bp, 2)
+        self.u = [e(T, 2, Bp, 1), e(T, 2, Bp, 1)]      # control planes (tau1, tau2)
+        self.K1 = e(T, 2, Bp, 2)                       # gain row 1, pairs
+        self.cs = e(T, 1, Bp, 2)                       # (c1 = u1 - K1 x, sigma1), pairs
         self.cost, self.dJ, self.smax, self.gamma = e(Bp), e(Bp), e(Bp), e(Bp)
         i32 = torch.int32
         self.status, self.n_iter, self.res_buf, self.n_roll = (e(Bp, dt=i32) for _ in range(4))
@@ -83,12 +83,12 @@ class BatchedNewtonSolver:
         self.hist_len = int(hist_len)
         self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
         self.hist_smax = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
-        self.K1.zero_(); self.sigma.zero_()
+        self.K1.zero_(); self.cs.zero_()
         b = _lib.GymBatch()
         b.B, b.Bp, b.N, b.hist_len = self.B, self.Bp, self.N, self.hist_len
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
-        for name in ("K1", "sigma", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
+        for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
                      "retry_list", "counters", "cand_ok", "partials", "stats"):
             setattr(b, name, getattr(self, name).data_ptr())
         b.x_ref, b.u_ref = self.x_ref.data_ptr(), self.u_ref.data_ptr()
@@ -156,10 +156,17 @@ class BatchedNewtonSolver:
         u = torch.empty((B, T, 2), dtype=F64, device=dev)
         K = torch.empty((B, T, 2, 4), dtype=F64, device=dev)
         s = torch.empty((B, T, 2), dtype=F64, device=dev)
-        _lib.check(self.eng.lib.gym_newton_finalize(C.byref(self.batch), self.k, x.data_ptr(), u.data_ptr(),
-                                                    K.data_ptr(), s.data_ptr(), self.eng.stream),
+        _lib.check(self.eng.lib.gym_newton_finalize(C.byref(self.eng._w), C.byref(self.batch), self.k, x.data_ptr(),
+                                                    u.data_ptr(), K.data_ptr(), s.data_ptr(), self.eng.stream),
                    "gym_newton_finalize")
         return x, u, K, s
+
+    def sigma(self) -> torch.Tensor:
+        """sigma (B,T,2) of every lane's most recent backward sweep."""
+        s = torch.empty((self.B, self.T, 2), dtype=F64, device=self.eng.device)
+        _lib.check(self.eng.lib.gym_newton_sigma(C.byref(self.eng._w), C.byref(self.batch), s.data_ptr(),
+                                                 self.eng.stream), "gym_newton_sigma")
+        return s
 
     # --- full solve ----------------------------------------------------------------------
     def solve(self, x0, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,

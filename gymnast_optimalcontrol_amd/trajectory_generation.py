@@ -205,7 +205,7 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
         return eng.unpack(solver.x[buf], 1)[0].cpu().numpy()
 
     def lane_sigma():
-        return eng.unpack(solver.sigma, 1)[0].cpu().numpy()
+        return solver.sigma()[0].cpu().numpy()
 
     x_traj = lane_x(0)
     assert x_traj.shape[0] == x_ref.shape[0], \

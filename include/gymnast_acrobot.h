@@ -19,14 +19,15 @@
  * Layouts
  *   lane-major  : the reference's own arrays stacked over lanes: x (B,N,4), u (B,T,2),
  *                 K (B,T,2,4), sigma (B,T,2), row-major.
- *   SoA "pairs" : time-major, lane-innermost, two components per 16-byte element so that a
- *                 wavefront reads 1 KiB contiguous per load instruction:
- *                   states  x   : (N, 2, Bp) double2   pairs (th1,th2), (w1,w2)
- *                   controls u  : (T, Bp)    double2   (tau1, tau2)
- *                   gains   K1  : (T, 2, Bp) double2   row 1 of K_t (row 0 is identically 0)
- *                   gains   Kf  : (T, 4, Bp) double2   full K_t, pairs (K00,K01)(K02,K03)(K10,K11)(K12,K13)
- *                   sigma   s   : (T, Bp)    double2
- *                 Bp = lane stride (>= B, multiple of 64).
+ *   SoA         : time-major, lane innermost (lane stride Bp >= B, a multiple of 64):
+ *     pairs  (W = 2): two fp64 components per 16-byte element, one 1 KiB load per wavefront
+ *                   states   x  : (N, 2, Bp) double2   (th1, th2), (w1, w2)
+ *                   gains    K1 : (T, 2, Bp) double2   row 1 of K_t (row 0 is identically 0)
+ *                   gains    Kf : (T, 4, Bp) double2   full K_t: (K00,K01)(K02,K03)(K10,K11)(K12,K13)
+ *                   offsets  cs : (T, Bp)    double2   (c1 = u1 - K1 x, sigma1) of the solver's sweep
+ *     planes (W = 1): one component per element
+ *                   controls u  : (T, 2, Bp) double    planes tau1, tau2
+ *                   sigma    s  : (T, 2, Bp) double
  */
 #ifndef GYMNAST_ACROBOT_H
 #define GYMNAST_ACROBOT_H
@@ -86,9 +87,9 @@ typedef struct gym_batch {
     int64_t B, Bp;      /* lanes, lane stride (multiple of 64)                     */
     int32_t N, hist_len;/* knots (T = N-1); rows of the optional history buffers   */
     double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered   */
-    double* u[2];       /* (T,Bp)   double2 control trajectories                  */
+    double* u[2];       /* (T,2,Bp) control planes, double-buffered               */
     double* K1;         /* (T,2,Bp) double2 feedback gains, row 1                 */
-    double* sigma;      /* (T,Bp)   double2 feed-forward                          */
+    double* cs;         /* (T,Bp)   double2 (c1 = u1 - K1 x, sigma1) of the sweep  */
     const double* x_ref;/* (N,4) shared reference states                          */
     const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
     double* cost;       /* (Bp) current J_k                                       */
@@ -127,22 +128,23 @@ int gym_stage_cost_derivs(const double* x, const double* xr, const double* u, co
                           const double R[4], int32_t terminal, double* l, double* gx, double* gu, int64_t n, void* stream);
 
 /* ---------------- layout transposes ---------------- */
-/* lane-major (B,L,C) -> SoA (L,C/2,Bp) double2; C even.  Padding lanes are zero-filled. */
-int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, void* stream);
+/* lane-major (B,L,C) -> SoA (L, C/W, Bp, W), W = 2 (pairs) or 1 (planes).  Padding lanes are zero-filled. */
+int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, int32_t W,
+                   void* stream);
 /* SoA -> lane-major; if sel != NULL lane b reads from (sel[b] ? src1 : src0). */
 int gym_unpack_lanes(const double* src0, const double* src1, const int32_t* sel, double* dst, int64_t B, int64_t Bp,
-                     int32_t L, int32_t C, void* stream);
+                     int32_t L, int32_t C, int32_t W, void* stream);
 /* compact gains K1 (T,2,Bp) -> full lane-major K (B,T,2,4) with row 0 = 0 */
 int gym_unpack_gains(const double* K1, double* K, int64_t B, int64_t Bp, int32_t T, void* stream);
 
 /* ---------------- trajectory kernels (SoA) ---------------- */
-/* trajectory_generation.py:74-87 simulate_open_loop: x0 (B,4) lane-major, u (T,Bp) SoA -> x (N,2,Bp);
+/* trajectory_generation.py:74-87 simulate_open_loop: x0 (B,4) lane-major, u (T,2,Bp) planes -> x (N,2,Bp);
  * if cost != NULL also total_cost (:231-252) of (x,u) with diagonal weights. */
 int gym_rollout_open_loop(const gym_model* m, const gym_weights* w, const double* x0, const double* u,
                           const double* x_ref, const double* u_ref, double* x, double* cost, int64_t B, int64_t Bp,
                           int32_t N, void* stream);
 /* trajectory_generation.py:218-229 forward_closed_loop_update with FULL gains Kf (T,4,Bp) and per-lane gamma (Bp);
- * writes x_new (N,2,Bp), u_new (T,Bp); cost (Bp) of the new trajectory if non-NULL. */
+ * u, sigma, u_new planes (T,2,Bp); writes x_new (N,2,Bp), u_new; cost (Bp) of the new trajectory if non-NULL. */
 int gym_closed_loop(const gym_model* m, const gym_weights* w, const double* x, const double* u, const double* Kf,
                     const double* sigma, const double* gamma, const double* x_ref, const double* u_ref,
                     double* x_new, double* u_new, double* cost, int64_t B, int64_t Bp, int32_t N, void* stream);
@@ -151,7 +153,7 @@ int gym_total_cost(const double* x, const double* u, const double* x_ref, const 
                    const double R[4], const double QT[16], double* cost, int64_t B, int64_t Bp, int32_t N, void* stream);
 /* Fused backward sweep = compute_costate_trajectory (:138-159) + build_stage_lists (:166-181) +
  * calculate_K_and_sigma (:183-216) for the Gauss-Newton blocks (2Q, 2R, S = 0, terminal 2Q_T):
- * K1 (T,2,Bp), sigma (T,Bp), dJ (Bp), smax = max|sigma| (Bp); lambda (N,2,Bp) costates if non-NULL. */
+ * K1 (T,2,Bp), sigma planes (T,2,Bp), dJ (Bp), smax = max|sigma| (Bp); lambda (N,2,Bp) costates if non-NULL. */
 int gym_backward_sweep(const gym_model* m, const gym_weights* w, const double* x, const double* u,
                        const double* x_ref, const double* u_ref, double* K1, double* sigma, double* dJ, double* smax,
                        double* lambda, int64_t B, int64_t Bp, int32_t N, void* stream);
@@ -169,7 +171,7 @@ int gym_riccati_general(const double* A, const double* Bm, const double* Q, cons
 /* ---------------- batched Newton / Armijo solver (newton_Algorithm, :298-398) ---------------- */
 /* Open-loop init (u = 0, :311-312), J_0 (:319), status/counters reset.  x0 (B,4) lane-major. */
 int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, const gym_batch* bt, void* stream);
-/* One outer iteration k for every ACTIVE lane: backward sweep, Armijo trial 1 (gamma0) fused with its cost,
+/* One outer iteration k for every ACTIVE lane: backward sweep (K1, cs), Armijo trial 1 (gamma0) fused with its cost,
  * parallel candidate rollouts gamma0*beta^j (j = 1..max_ls-1) for lanes that rejected trial 1, accepted-
  * candidate rollout, lane status update, then device statistics into bt->stats:
  *   [0] lanes still active  [1] sum J over lanes  [2] sum max|sigma|^2 over lanes that ran
@@ -179,9 +181,12 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
 int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt,
                          int32_t k, void* stream);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
- * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) (last iteration's gains), sigma_out (B,T,2). Any output may be NULL. */
-int gym_newton_finalize(const gym_batch* bt, int32_t k_done, double* x_out, double* u_out, double* K_out,
-                        double* sigma_out, void* stream);
+ * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
+ * (sigma0 recomputed from that iteration's u0).  Any output may be NULL. */
+int gym_newton_finalize(const gym_weights* w, const gym_batch* bt, int32_t k_done, double* x_out, double* u_out,
+                        double* K_out, double* sigma_out, void* stream);
+/* sigma (B,T,2) of each lane's most recent backward sweep (sigma1 from cs, sigma0 recomputed). */
+int gym_newton_sigma(const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);
 
 /* [host] create / destroy the events of a gym_timing; collect = add the elapsed time of every pending
  * pair (call only after the stream that recorded them has been synchronised). */

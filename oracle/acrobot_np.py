@@ -211,63 +211,95 @@ def closed_loop(x, u, K, sig, gamma, pset=1):
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS = 0, 1, 2, 3
 
 
+class NewtonStepper:
+    """One outer iteration of newton_Algorithm (trajectory_generation.py:329-396) per call, for every lane.
+
+    Same per-lane semantics as the reference: u-ref trim (:301-306), u0 = 0 open-loop init (:311-312),
+    Armijo with strict '<' (:361) and gamma *= beta (:365), LS failure -> stop without update (:367-369),
+    update then stop on max|sigma| < tol (:383-396).  ``iteration()`` returns the 8 statistics the HIP
+    solver reports (gymnast_optimalcontrol_amd.solver.STAT_FIELDS), so the multi-rank loop logic can be
+    exercised on CPU with this oracle as the per-shard engine."""
+
+    def __init__(self, x0, x_ref, u_ref, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0, max_ls=20,
+                 Q=Q_DEFAULT, R=R_DEFAULT, QT=QT_DEFAULT, pset=1):
+        x0 = np.atleast_2d(np.asarray(x0, float))
+        u_ref = np.asarray(u_ref, float)
+        if u_ref.shape[0] == x_ref.shape[0]:
+            u_ref = u_ref[:-1]
+        if u_ref.shape[0] != x_ref.shape[0] - 1:
+            raise ValueError("Incompatible dimensions")
+        self.x_ref, self.u_ref = np.asarray(x_ref, float), u_ref
+        self.tol, self.beta, self.c, self.gamma_0, self.max_ls = tol, beta, c, gamma_0, max_ls
+        self.Q, self.R, self.QT, self.pset = Q, R, QT, pset
+        Bn = x0.shape[0]
+        self.u = np.zeros((Bn,) + u_ref.shape)
+        self.x = simulate_open_loop(x0, self.u, pset)
+        self.J = total_cost(self.x, self.u, self.x_ref, u_ref, Q, R, QT)
+        self.status = np.full(Bn, ACTIVE); self.n_iter = np.zeros(Bn, int); self.n_roll = np.zeros(Bn, int)
+        self.K = np.zeros((Bn, u_ref.shape[0], 2, 4)); self.sig = np.zeros((Bn, u_ref.shape[0], 2))
+        self.smax = np.zeros(Bn)
+        self.cost_hist = [self.J.copy()]; self.signorm_hist = []
+        self.k = 0
+
+    def iteration(self):
+        Q, R, QT, pset = self.Q, self.R, self.QT, self.pset
+        x, u, J, Bn = self.x, self.u, self.J, self.x.shape[0]
+        ia = np.nonzero(self.status == ACTIVE)[0]
+        sn = np.full(Bn, np.nan); ch = np.full(Bn, np.nan)
+        n_retry = 0
+        if ia.size:
+            A_d, B_d, q, r, QTb, qT = stage_lists(x[ia], u[ia], self.x_ref, self.u_ref, Q, R, QT, pset)
+            Ka, sa, dJ = riccati(A_d, B_d, 2 * Q, 2 * R, np.zeros((2, 4)), q, r, QTb, qT)
+            self.K[ia] = Ka; self.sig[ia] = sa
+            smax = np.max(np.abs(sa), axis=(1, 2))
+            self.smax[ia] = smax; sn[ia] = smax
+            gam = np.full(ia.size, float(self.gamma_0))
+            done = np.zeros(ia.size, bool); ok = np.zeros(ia.size, bool)
+            xn_acc = x[ia].copy(); un_acc = u[ia].copy(); Jn_acc = J[ia].copy()
+            for i in range(self.max_ls):
+                todo = np.nonzero(~done)[0]
+                if todo.size == 0:
+                    break
+                if i == 1:
+                    n_retry = todo.size
+                xn, un = closed_loop(x[ia[todo]], u[ia[todo]], Ka[todo], sa[todo], gam[todo], pset)
+                Jn = total_cost(xn, un, self.x_ref, self.u_ref, Q, R, QT)
+                self.n_roll[ia[todo]] += 1
+                acc = Jn < J[ia[todo]] + self.c * gam[todo] * dJ[todo]
+                sel = todo[acc]
+                xn_acc[sel] = xn[acc]; un_acc[sel] = un[acc]; Jn_acc[sel] = Jn[acc]
+                ok[sel] = True; done[sel] = True
+                gam[todo[~acc]] *= self.beta
+            self.n_iter[ia] += 1
+            self.status[ia[~ok]] = LS_FAILED
+            good = ia[ok]
+            x[good] = xn_acc[ok]; u[good] = un_acc[ok]; J[good] = Jn_acc[ok]
+            self.status[ia[ok & (smax < self.tol)]] = CONVERGED
+            ch[good] = J[good]
+        self.signorm_hist.append(sn); self.cost_hist.append(ch)
+        ran = self.n_iter == self.k + 1
+        self.k += 1
+        return np.array([np.sum(self.status == ACTIVE), np.sum(J), np.sum(self.smax[ran] ** 2), np.sum(ran),
+                         n_retry, np.sum(self.status == CONVERGED), np.sum(self.status == LS_FAILED),
+                         np.sum(self.n_roll)], dtype=float)
+
+    def result(self):
+        status = self.status.copy()
+        status[status == ACTIVE] = MAX_ITERS
+        return dict(x=self.x, u=self.u, K=self.K, sigma=self.sig, n_iter=self.n_iter, status=status, cost=self.J,
+                    n_rollouts=self.n_roll, cost_hist=np.array(self.cost_hist),
+                    sigma_norm_hist=np.array(self.signorm_hist))
+
+
 def newton_solve(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0, max_ls=20,
                  Q=Q_DEFAULT, R=R_DEFAULT, QT=QT_DEFAULT, pset=1):
-    """Per-lane semantics of newton_Algorithm (trajectory_generation.py:298-398), vectorised.
-
-    Every lane follows the reference's control flow on its own: u-ref trim (:301-306), u0 = 0
-    open-loop init (:311-312), Armijo with strict '<' (:361) and gamma *= beta (:365), LS failure
-    -> stop without update (:367-369), update then stop on max|sigma| < tol (:383-396).
-    Returns dict with x (B,N,4), u (B,T,2), K, sigma (last iteration), n_iter, status, cost history.
-    """
-    x0 = np.atleast_2d(np.asarray(x0, float))
-    u_ref = np.asarray(u_ref, float)
-    if u_ref.shape[0] == x_ref.shape[0]:
-        u_ref = u_ref[:-1]
-    if u_ref.shape[0] != x_ref.shape[0] - 1:
-        raise ValueError("Incompatible dimensions")
-    Bn = x0.shape[0]
-    u = np.zeros((Bn,) + u_ref.shape)
-    x = simulate_open_loop(x0, u, pset)
-    J = total_cost(x, u, x_ref, u_ref, Q, R, QT)
-    status = np.full(Bn, ACTIVE); n_iter = np.zeros(Bn, int); n_roll = np.zeros(Bn, int)
-    K = np.zeros((Bn, u.shape[1], 2, 4)); sig = np.zeros((Bn, u.shape[1], 2))
-    cost_hist = [J.copy()]; signorm_hist = []
+    """Per-lane semantics of newton_Algorithm (trajectory_generation.py:298-398), vectorised over lanes."""
+    st = NewtonStepper(x0, x_ref, u_ref, tol, beta, c, gamma_0, max_ls, Q, R, QT, pset)
     for _k in range(max_iters):
-        act = status == ACTIVE
-        if not act.any():
+        if not (st.status == ACTIVE).any():
             break
-        ia = np.nonzero(act)[0]
-        A_d, B_d, q, r, QTb, qT = stage_lists(x[ia], u[ia], x_ref, u_ref, Q, R, QT, pset)
-        Ka, sa, dJ = riccati(A_d, B_d, 2 * Q, 2 * R, np.zeros((2, 4)), q, r, QTb, qT)
-        K[ia] = Ka; sig[ia] = sa
-        smax = np.max(np.abs(sa), axis=(1, 2))
-        sn = np.full(Bn, np.nan); sn[ia] = smax; signorm_hist.append(sn)
-        gam = np.full(ia.size, float(gamma_0))
-        done = np.zeros(ia.size, bool); ok = np.zeros(ia.size, bool)
-        xn_acc = x[ia].copy(); un_acc = u[ia].copy(); Jn_acc = J[ia].copy()
-        for _i in range(max_ls):
-            todo = np.nonzero(~done)[0]
-            if todo.size == 0:
-                break
-            xn, un = closed_loop(x[ia[todo]], u[ia[todo]], Ka[todo], sa[todo], gam[todo], pset)
-            Jn = total_cost(xn, un, x_ref, u_ref, Q, R, QT)
-            n_roll[ia[todo]] += 1
-            acc = Jn < J[ia[todo]] + c * gam[todo] * dJ[todo]
-            sel = todo[acc]
-            xn_acc[sel] = xn[acc]; un_acc[sel] = un[acc]; Jn_acc[sel] = Jn[acc]
-            ok[sel] = True; done[sel] = True
-            gam[todo[~acc]] *= beta
-        n_iter[ia] += 1
-        status[ia[~ok]] = LS_FAILED
-        good = ia[ok]
-        x[good] = xn_acc[ok]; u[good] = un_acc[ok]; J[good] = Jn_acc[ok]
-        conv = ok & (smax < tol)
-        status[ia[conv]] = CONVERGED
-        ch = np.full(Bn, np.nan); ch[good] = J[good]; cost_hist.append(ch)
-    status[status == ACTIVE] = MAX_ITERS
-    return dict(x=x, u=u, K=K, sigma=sig, n_iter=n_iter, status=status, cost=J, n_rollouts=n_roll,
-                cost_hist=np.array(cost_hist), sigma_norm_hist=np.array(signorm_hist))
+        st.iteration()
+    return st.result()
 
 
 def load_task2_refs(path):

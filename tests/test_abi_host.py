@@ -69,9 +69,10 @@ def test_launchers_reject_bad_arguments_without_a_device():
     """Argument validation happens on the host before any launch."""
     from gymnast_optimalcontrol_amd import _lib
     lib = _lib.load()
-    assert lib.gym_pack_lanes(None, None, 4, 64, 3, 4, None) == 1
-    assert lib.gym_pack_lanes(1, 1, 4, 60, 3, 4, None) == 1        # Bp not a multiple of 64
-    assert lib.gym_pack_lanes(1, 1, 4, 64, 3, 3, None) == 1        # odd component count
+    assert lib.gym_pack_lanes(None, None, 4, 64, 3, 4, 2, None) == 1
+    assert lib.gym_pack_lanes(1, 1, 4, 60, 3, 4, 2, None) == 1     # Bp not a multiple of 64
+    assert lib.gym_pack_lanes(1, 1, 4, 64, 3, 3, 2, None) == 1     # odd component count for pairs
+    assert lib.gym_pack_lanes(1, 1, 4, 64, 3, 4, 3, None) == 1     # element width must be 1 or 2
     assert lib.gym_newton_iteration(None, None, None, None, 0, None) == 1
     b = _lib.GymBatch()
     assert lib.gym_newton_init(None, None, None, C.byref(b), None) == 1

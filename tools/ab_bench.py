@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of library variants in ONE process on one device (measurement tool).
+
+    python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so ...
+Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
+kernel library is swapped), so buffer placement -- worth +-4% on its own -- is held fixed; prints
+per-variant median backward / trial kernel times and whole-solve throughput.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--batch", type=int, default=262144)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--max-iters", type=int, default=5000)
+    a = ap.parse_args()
+    import torch
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    x_ref, u_ref = load_refs()
+    x0 = make_x0(a.batch)
+    from gymnast_optimalcontrol_amd import _lib
+    eng = AcrobotEngine(lib_path=os.path.abspath(a.libs[0]))
+    s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1).enable_timing()
+    xd = eng.t(x0)
+    libs = {p: _lib.load(os.path.abspath(p)) for p in a.libs}
+    res = {p: {"bwd": [], "trial": [], "its": [], "sec": []} for p in a.libs}
+    for r in range(a.rounds + 1):
+        for p in a.libs:
+            eng.lib = libs[p]
+            s.reset_timing()
+            out = s.solve(xd, a.max_iters)
+            kt = s.kernel_times()
+            if r == 0:
+                continue   # warm-up round
+            res[p]["bwd"].append(kt["backward"][0] / kt["backward"][1])
+            res[p]["trial"].append(kt["trial"][0] / kt["trial"][1])
+            res[p]["its"].append(out.lane_iterations / out.seconds)
+            res[p]["sec"].append(out.seconds)
+    for p in a.libs:
+        d = res[p]
+        print(json.dumps({"lib": os.path.basename(p), "bwd_ms": float(np.median(d["bwd"])),
+                          "trial_ms": float(np.median(d["trial"])), "Mits": float(np.median(d["its"])) / 1e6,
+                          "bwd_all": [round(v, 4) for v in d["bwd"]], "trial_all": [round(v, 4) for v in d["trial"]]}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: smoke -> parity tests -> short bench.  Every GPU step has its own time limit;
+# a fault / abort / timeout (exit codes other than 0 and 1) ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] end $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  if grep -q -i -E "illegal memory access|memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
+    echo "GPU fault in $name: stopping"; exit 3
+  fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    smoke)  step smoke 400 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests)  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --tb=short ;;
+    bench)  step bench 600 python -u bench.py --steps 1 --warmup 1 --cpu-lanes 4096 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
