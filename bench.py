@@ -34,15 +34,18 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
 
 
 def algorithmic_bytes(N: int) -> dict:
-    """Compulsory HBM bytes per lane per launch (fp64), see DESIGN.md section 4.
+    """Compulsory HBM bytes per lane for one pass of each solver kernel (fp64), see DESIGN.md section 4.
 
-    backward: read x (4N) + u (2T); write K row 1 (4T) + sigma (2T)      (K row 0 == 0 is not stored)
-    trial   : read x (4T... the whole x is needed for dx, 4N) + u (2T) + K1 (4T) + sigma (2T);
-              write x_new (4N) + u_new (2T)
+    backward sweep : read x (4N) + u (2T);            write K row 1 (4T) + (c1, sigma1) (2T)
+    Armijo trial   : read K row 1 (4T) + (c1, sigma1) (2T) + u0 (T) + x_0 (4);
+                     write x_new (4N) + u_new (2T)
+    A Newton iteration of one lane is one sweep + one trial (no backtracking) = 100,096 B at N = 501.
+    (SURVEY.md 8(d)'s 152,096 B is the reference's data flow: K stored 2x4 and the trial re-reading x, u.)
     """
     T = N - 1
-    return {"backward": 8 * (4 * N + 2 * T + 4 * T + 2 * T),
-            "trial": 8 * (4 * N + 2 * T + 4 * T + 2 * T + 4 * N + 2 * T),
+    bwd = 8 * (4 * N + 2 * T + 4 * T + 2 * T)
+    trial = 8 * (4 * T + 2 * T + T + 4 + 4 * N + 2 * T)
+    return {"backward": bwd, "trial": trial, "iteration": bwd + trial,
             "survey_per_iteration": 8 * ((4 * N + 2 * T) + 10 * T + (2 * (4 * N + 2 * T) + 10 * T))}
 
 
@@ -158,26 +161,43 @@ def main():
         for kind, (ms, launches) in kt.items():
             if launches:
                 kern[kind] = {"avg_ms": ms / launches, "launches": launches}
-        # lanes processed per launch: every lane runs the backward sweep and trial 1 each iteration it is active
-        lane_launch = lane_its / max(1, kt["trial"][1]) if kt["trial"][1] else 0
-        for kind in ("backward", "trial"):
-            if kind in kern:
-                by = ab[kind] * lane_launch
-                kern[kind]["algorithmic_bytes_per_launch"] = by
-                kern[kind]["achieved_GBs"] = by / (kern[kind]["avg_ms"] * 1e-3) / 1e9
-        dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
-        traffic = None
+        if "phase_odd" in kern:
+            # pipelined schedule: every lane-iteration = one sweep + one trial, all inside the phase launches
+            # (2 * iterations + 1 per solve; a launch's time is recorded whenever its timing slot is free)
+            dom = "phase"
+            rec_ms = sum(kern[k]["avg_ms"] * kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
+            rec_n = sum(kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
+            total_launches = a.steps * (2 * n_iters_outer + 1)
+            per_launch = lane_its * ab["iteration"] / total_launches
+            kern["phase"] = {"avg_ms": rec_ms / rec_n, "launches": total_launches, "recorded": rec_n,
+                             "algorithmic_bytes_per_launch": per_launch}
+            kern["phase"]["achieved_GBs"] = per_launch / (kern["phase"]["avg_ms"] * 1e-3) / 1e9
+            bytes_per_lane, unit_note = ab["iteration"], "sweep + trial of one lane-iteration"
+        else:
+            for kind in ("backward", "trial"):
+                if kind in kern:
+                    per_launch = lane_its * ab[kind] / kern[kind]["launches"]
+                    kern[kind]["algorithmic_bytes_per_launch"] = per_launch
+                    kern[kind]["achieved_GBs"] = per_launch / (kern[kind]["avg_ms"] * 1e-3) / 1e9
+            dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
+            bytes_per_lane, unit_note = ab[dom], f"one {dom} pass of one lane"
+        traffic, traffic_ratio = None, None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):
+        if os.path.exists(tfile):      # committed rocprofv3 --pmc measurement (tools/profile.sh, parse_profiles.py)
             try:
-                traffic = json.load(open(tfile)).get(dom, {}).get("hbm_bytes_per_launch")
+                t = json.load(open(tfile)).get(dom, {})
+                traffic, traffic_ratio = t.get("hbm_bytes_per_launch"), t.get("traffic_over_algorithmic")
             except Exception:
                 traffic = None
         ach = kern[dom]["achieved_GBs"]
         out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                           "bytes_per_lane": ab[dom], "lanes_per_launch": lane_launch}
+                           "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
+                           "traffic_source": "profiles/pmc_traffic.json (rocprofv3 PMC, 20-iteration run, all lanes "
+                                             "active)", "bytes_per_unit": bytes_per_lane,
+                           "unit_of_work": unit_note, "algorithmic_bytes_per_launch":
+                           kern[dom]["algorithmic_bytes_per_launch"]}
         out["kernels"] = kern
+        out["schedule"] = "pipelined" if solver.pipeline else "serial"
     if parity is not None:
         out["parity"] = parity
     if rank == 0 and world == 1 and not a.no_cpu:

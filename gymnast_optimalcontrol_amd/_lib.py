@@ -21,10 +21,11 @@ EXPORTS = (
     "gym_pack_lanes", "gym_unpack_lanes", "gym_unpack_gains",
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
     "gym_riccati_general",
-    "gym_newton_init", "gym_newton_iteration", "gym_newton_finalize", "gym_newton_sigma",
+    "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase",
+    "gym_newton_finalize", "gym_newton_sigma",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
-KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats")
+KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even")
 
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4
 STATUS_NAMES = {ACTIVE: "active", CONVERGED: "converged", LS_FAILED: "ls_failed", MAX_ITERS: "max_iters", PAD: "pad"}
@@ -47,7 +48,7 @@ _P = C.c_void_p
 
 
 class GymTiming(C.Structure):
-    _fields_ = [("ev", _P * 10), ("ms", C.c_double * 5), ("launches", C.c_int64 * 5), ("pending", C.c_int32),
+    _fields_ = [("ev", _P * 14), ("ms", C.c_double * 7), ("launches", C.c_int64 * 7), ("pending", C.c_int32),
                 ("pad", C.c_int32)]
 
 
@@ -80,6 +81,8 @@ _SIGS = {
     "gym_riccati_general": [_P] * 12 + [_I64, _I64, _I32, _P],
     "gym_newton_init": [_MP, _WP, _P, _BP, _P],
     "gym_newton_iteration": [_MP, _WP, _AP, _BP, _I32, _P],
+    "gym_newton_pipeline_split": [_BP, C.POINTER(C.c_int64)],
+    "gym_newton_phase": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_finalize": [_WP, _BP, _I32, _P, _P, _P, _P, _P],
     "gym_newton_sigma": [_WP, _BP, _P, _P],
     "gym_timing_create": [C.POINTER(GymTiming)],

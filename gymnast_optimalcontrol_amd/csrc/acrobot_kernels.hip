@@ -654,22 +654,37 @@ __global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const
                                  x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
 }
 
+// Lane ranges: the serial schedule runs every lane [0, B); the pipelined schedule splits the batch
+// into two halves H0 = [0, Bh), H1 = [Bh, B) whose iterations are offset by one phase.
+struct Range {
+    int64_t lo, hi;
+};
+
+__device__ __forceinline__ void backward_solver(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+                                                const double* __restrict__ u, const double* __restrict__ xr,
+                                                const double* __restrict__ ur, double2* __restrict__ K1,
+                                                double2* __restrict__ cs, double* __restrict__ dJ,
+                                                double* __restrict__ smax, double* __restrict__ hist_smax, int64_t l,
+                                                int64_t Bp, int N, int k, int hist_len) {
+    double d, s;
+    backward_lane<true, false>(m, w, x, u, xr, ur, K1, cs, nullptr, nullptr, l, Bp, N, d, s);
+    dJ[l] = d;
+    smax[l] = s;
+    if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
+}
+
 __global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weights w, const double2* __restrict__ x,
                                                         const double* __restrict__ u, const double* __restrict__ xr,
                                                         const double* __restrict__ ur, double2* __restrict__ K1,
                                                         double2* __restrict__ cs, double* __restrict__ dJ,
                                                         double* __restrict__ smax,
                                                         const int32_t* __restrict__ status,
-                                                        double* __restrict__ hist_smax, int64_t B, int64_t Bp, int N,
+                                                        double* __restrict__ hist_smax, Range rg, int64_t Bp, int N,
                                                         int k, int hist_len) {
-    const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
-    if (l >= B || status[l] != GYM_ACTIVE) return;
+    const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
+    if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
     const Dyn m(mm);
-    double d, s;
-    backward_lane<true, false>(m, w, x, u, xr, ur, K1, cs, nullptr, nullptr, l, Bp, N, d, s);
-    dJ[l] = d;
-    smax[l] = s;
-    if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
+    backward_solver(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len);
 }
 
 struct SolverCtl {
@@ -694,48 +709,94 @@ __device__ __forceinline__ void fail_lane(const SolverCtl& a, int64_t l, int32_t
     res_buf[l] = a.k & 1;
 }
 
-// Armijo trial 1 (gamma0) fused with the candidate rollout and its cost.
-__global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a,
-                                                     const double2* __restrict__ x, const double* __restrict__ u,
-                                                     const double2* __restrict__ K1, const double2* __restrict__ cs,
-                                                     const double* __restrict__ xr, const double* __restrict__ ur,
-                                                     double2* __restrict__ xn, double* __restrict__ un,
-                                                     double* __restrict__ cost, const double* __restrict__ dJ,
-                                                     const double* __restrict__ smax, double* __restrict__ gamma,
-                                                     int32_t* __restrict__ status, int32_t* __restrict__ n_iter,
-                                                     int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
-                                                     int32_t* __restrict__ retry_list, int32_t* __restrict__ counters,
-                                                     double* __restrict__ hist_cost, int64_t B, int64_t Bp, int N) {
-    const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
-    if (l >= B || status[l] != GYM_ACTIVE) return;
-    const Dyn m(mm);
-    const double2 xa = x[l], xb = x[Bp + l];
+// The per-lane state and streams one Armijo trial touches.
+struct TrialIO {
+    const double2* x;   // current trajectory (only x_0 is read)
+    const double* u;    // current control planes (u0 is read)
+    double2* xn;        // candidate trajectory (written)
+    double* un;         // candidate controls (written)
+};
+
+// Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass).
+__device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w, const SolverCtl& a, const TrialIO& io,
+                                             const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                             const double* __restrict__ xr, const double* __restrict__ ur,
+                                             double* __restrict__ cost, const double* __restrict__ dJ,
+                                             const double* __restrict__ smax, double* __restrict__ gamma,
+                                             int32_t* __restrict__ status, int32_t* __restrict__ n_iter,
+                                             int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
+                                             int32_t* __restrict__ retry_list, int32_t* __restrict__ counter,
+                                             double* __restrict__ hist_cost, int64_t l, int64_t Bp, int N) {
+    const double2 xa = io.x[l], xb = io.x[Bp + l];
     const double g = a.gamma0;
-    const double Jn = rollout_cform<true>(m, w, u, K1, cs, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+    const double Jn = rollout_cform<true>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y, xb.x,
+                                          xb.y);
     n_roll[l] += 1;
     if (Jn < cost[l] + a.c * g * dJ[l]) {  // strict Armijo test (:361)
         n_iter[l] += 1;
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     } else if (a.max_ls > 1) {
-        const int idx = atomicAdd(&counters[0], 1);
-        retry_list[idx] = (int32_t)l;
+        retry_list[atomicAdd(counter, 1)] = (int32_t)l;
     } else {
         n_iter[l] += 1;
         fail_lane(a, l, status, res_buf);
     }
 }
 
+__global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+                                                     const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                     const double* __restrict__ xr, const double* __restrict__ ur,
+                                                     double* __restrict__ cost, const double* __restrict__ dJ,
+                                                     const double* __restrict__ smax, double* __restrict__ gamma,
+                                                     int32_t* __restrict__ status, int32_t* __restrict__ n_iter,
+                                                     int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
+                                                     int32_t* __restrict__ retry_list, int32_t* __restrict__ counter,
+                                                     double* __restrict__ hist_cost, Range rg, int64_t Bp, int N) {
+    const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
+    if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
+    const Dyn m(mm);
+    trial_solver(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+                 retry_list + rg.lo, counter, hist_cost, l, Bp, N);
+}
+
+// One pipeline phase: the first nb_b workgroups run the backward sweep of one half, the rest run the
+// Armijo trial of the other half.  The sweep is HBM-bound and the trial fp64-VALU-bound, so co-resident
+// waves of the two kinds overlap memory and arithmetic on every CU.  The two halves' lanes are disjoint.
+__global__ __launch_bounds__(BLK, 4) void k_nt_phase(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+                                                     const double2* __restrict__ xb_in,
+                                                     const double* __restrict__ ub_in, int kb, int nb_b,
+                                                     Range rb, Range rt, double2* __restrict__ K1,
+                                                     double2* __restrict__ cs, const double* __restrict__ xr,
+                                                     const double* __restrict__ ur, double* __restrict__ cost,
+                                                     double* __restrict__ dJ, double* __restrict__ smax,
+                                                     double* __restrict__ gamma, int32_t* __restrict__ status,
+                                                     int32_t* __restrict__ n_iter, int32_t* __restrict__ res_buf,
+                                                     int32_t* __restrict__ n_roll, int32_t* __restrict__ retry_list,
+                                                     int32_t* __restrict__ counter, double* __restrict__ hist_cost,
+                                                     double* __restrict__ hist_smax, int64_t Bp, int N) {
+    const Dyn m(mm);
+    if ((int)blockIdx.x < nb_b) {
+        const int64_t l = rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
+        if (l >= rb.hi || status[l] != GYM_ACTIVE) return;
+        backward_solver(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len);
+    } else {
+        const int64_t l = rt.lo + (int64_t)(blockIdx.x - nb_b) * BLK + threadIdx.x;
+        if (l >= rt.hi || status[l] != GYM_ACTIVE) return;
+        trial_solver(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+                     retry_list + rt.lo, counter, hist_cost, l, Bp, N);
+    }
+}
+
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
-__global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights w, SolverCtl a,
-                                                       const double2* __restrict__ x, const double* __restrict__ u,
+__global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                        const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                        const double* __restrict__ xr, const double* __restrict__ ur,
                                                        const double* __restrict__ cost, const double* __restrict__ dJ,
                                                        const int32_t* __restrict__ retry_list,
-                                                       const int32_t* __restrict__ counters,
+                                                       const int32_t* __restrict__ counter,
                                                        uint8_t* __restrict__ cand_ok, int64_t Bp, int N) {
     const int nj = a.max_ls - 1;
-    const int64_t total = (int64_t)counters[0] * nj;
+    const int64_t total = (int64_t)(*counter) * nj;
     const Dyn m(mm);
     for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
         const int64_t r = i / nj;
@@ -743,27 +804,25 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights
         const int64_t l = retry_list[r];
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
-        const double2 xa = x[l], xb = x[Bp + l];
-        const double Jn = rollout_cform<false>(m, w, u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x, xa.y,
+        const double2 xa = io.x[l], xb = io.x[Bp + l];
+        const double Jn = rollout_cform<false>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x, xa.y,
                                                xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
     }
 }
 
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
-__global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, SolverCtl a,
-                                                  const double2* __restrict__ x, const double* __restrict__ u,
+__global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                   const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
-                                                  double2* __restrict__ xn, double* __restrict__ un,
                                                   double* __restrict__ cost, const double* __restrict__ smax,
                                                   double* __restrict__ gamma, int32_t* __restrict__ status,
                                                   int32_t* __restrict__ n_iter, int32_t* __restrict__ res_buf,
                                                   int32_t* __restrict__ n_roll, const int32_t* __restrict__ retry_list,
-                                                  const int32_t* __restrict__ counters,
+                                                  const int32_t* __restrict__ counter,
                                                   const uint8_t* __restrict__ cand_ok, double* __restrict__ hist_cost,
                                                   int64_t Bp, int N) {
-    const int nr = counters[0];
+    const int nr = *counter;
     const int nj = a.max_ls - 1;
     const Dyn m(mm);
     for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < nr; i += (int64_t)gridDim.x * BLK) {
@@ -780,8 +839,9 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, S
         n_roll[l] += jacc;
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
-        const double2 xa = x[l], xb = x[Bp + l];
-        const double Jn = rollout_cform<true>(m, w, u, K1, cs, xr, ur, xn, un, g, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+        const double2 xa = io.x[l], xb = io.x[Bp + l];
+        const double Jn = rollout_cform<true>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y, xb.x,
+                                              xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -798,12 +858,13 @@ __global__ __launch_bounds__(STAT_THREADS) void k_stats_partial(const int32_t* _
                                                                 const double* __restrict__ smax,
                                                                 const int32_t* __restrict__ n_iter,
                                                                 const int32_t* __restrict__ n_roll,
-                                                                double* __restrict__ partials, int64_t B, int k) {
+                                                                double* __restrict__ partials, Range rg, int k) {
     __shared__ double red[STAT_THREADS / 64][NSTAT];
     double acc[NSTAT] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int64_t chunk = (B + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = (int64_t)blockIdx.x * chunk;
-    const int64_t hi = (lo + chunk < B) ? lo + chunk : B;
+    const int64_t n = rg.hi - rg.lo;
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = rg.lo + (int64_t)blockIdx.x * chunk;
+    const int64_t hi = (lo + chunk < rg.hi) ? lo + chunk : rg.hi;
     for (int64_t l = lo + threadIdx.x; l < hi; l += STAT_THREADS) {
         const int st = status[l];
         const bool ran = n_iter[l] == k + 1;
@@ -829,17 +890,20 @@ __global__ __launch_bounds__(STAT_THREADS) void k_stats_partial(const int32_t* _
     }
 }
 
-__global__ void k_stats_final(const double* __restrict__ partials, int32_t* __restrict__ counters,
-                              double* __restrict__ stats, int nblocks) {
+// stats_out[0..7] = this range's statistics; if other != NULL, total[s] = other[s] + stats_out[s].
+__global__ void k_stats_final(const double* __restrict__ partials, int32_t* __restrict__ counter,
+                              double* __restrict__ stats_out, const double* __restrict__ other,
+                              double* __restrict__ total, int nblocks) {
     const int s = threadIdx.x;
     if (s < NSTAT) {
         double v = 0.0;
         for (int b = 0; b < nblocks; ++b) v += partials[(int64_t)b * NSTAT + s];
-        if (s == 4) v = (double)counters[0];
-        stats[s] = v;
+        if (s == 4) v = (double)(*counter);
+        stats_out[s] = v;
+        if (other) total[s] = other[s] + v;
     }
     __syncthreads();
-    if (s == 0) counters[0] = 0;  // the retry list is rebuilt every iteration
+    if (s == 0) *counter = 0;  // the retry list is rebuilt every iteration
 }
 
 __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restrict__ res_buf, int64_t B, int k_done) {
@@ -1044,55 +1108,110 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(b->counters, 0, sizeof(int32_t) * 4, st);
     if (e != hipSuccess) return (int)e;
+    e = hipMemsetAsync(b->stats, 0, sizeof(double) * 24, st);
+    if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, *m, *w, x0, b->u[0], b->x_ref, b->u_ref,
                        (double2*)b->x[0], b->cost, b->status, b->n_iter, b->res_buf, b->n_roll, b->gamma, b->smax,
                        b->dJ, b->B, b->Bp, b->N);
     return launch_status();
 }
 
-int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k,
-                         void* s) {
-    if (!m || !w || !a || bad_batch(b) || k < 0 || a->max_ls < 1 || (a->max_ls > 1 && !b->cand_ok)) return GYM_EINVAL;
-    hipStream_t st = (hipStream_t)s;
-    const int cur = k & 1, nxt = (k + 1) & 1;
-    const double2* x = (const double2*)b->x[cur];
-    const double* u = b->u[cur];
-    double2* xn = (double2*)b->x[nxt];
-    double* un = b->u[nxt];
+static void launch_post_trial(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
+                              const SolverCtl& c, const TrialIO& io, Range rg, int32_t* counter, double* stats_out,
+                              const double* other, double* total, hipStream_t st) {
+    const int64_t n = rg.hi - rg.lo;
     const double2* K1 = (const double2*)b->K1;
     const double2* cs = (const double2*)b->cs;
+    double* hc = a->record_history ? b->hist_cost : nullptr;
+    if (a->max_ls > 1 && n > 0) {
+        {
+            TimedLaunch tl(b->timing, 2, st);
+            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
+            hipLaunchKernelGGL(k_nt_candidates, dim3(gc), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref, b->u_ref,
+                               b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
+        }
+        TimedLaunch tl(b->timing, 3, st);
+        hipLaunchKernelGGL(k_nt_retry, dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref,
+                           b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
+                           b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
+    }
+    TimedLaunch tl(b->timing, 4, st);
+    hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
+                       b->n_iter, b->n_roll, b->partials, rg, c.k);
+    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64), 0, st, b->partials, counter, stats_out, other, total,
+                       STAT_BLOCKS);
+}
+
+static TrialIO trial_io(const gym_batch* b, int k) {
+    return TrialIO{(const double2*)b->x[k & 1], b->u[k & 1], (double2*)b->x[(k + 1) & 1], b->u[(k + 1) & 1]};
+}
+
+static bool bad_iter_args(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b) {
+    return !m || !w || !a || bad_batch(b) || a->max_ls < 1 || (a->max_ls > 1 && !b->cand_ok);
+}
+
+int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k,
+                         void* s) {
+    if (bad_iter_args(m, w, a, b) || k < 0) return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
+    const Range all{0, b->B};
+    const TrialIO io = trial_io(b, k);
     const int grid = grid_for(b->B, BLK);
     const bool hist = a->record_history != 0;
     {
         TimedLaunch tl(b->timing, 0, st);
-        hipLaunchKernelGGL(k_nt_backward, dim3(grid), dim3(BLK), 0, st, *m, *w, x, u, b->x_ref, b->u_ref,
+        hipLaunchKernelGGL(k_nt_backward, dim3(grid), dim3(BLK), 0, st, *m, *w, io.x, io.u, b->x_ref, b->u_ref,
                            (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
-                           hist ? b->hist_smax : nullptr, b->B, b->Bp, b->N, k, b->hist_len);
+                           hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
-    SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
-    double* hc = hist ? b->hist_cost : nullptr;
+    const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     {
         TimedLaunch tl(b->timing, 1, st);
-        hipLaunchKernelGGL(k_nt_trial, dim3(grid), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs, b->x_ref, b->u_ref, xn,
-                           un, b->cost, b->dJ, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
-                           b->retry_list, b->counters, hc, b->B, b->Bp, b->N);
+        hipLaunchKernelGGL(k_nt_trial, dim3(grid), dim3(BLK), 0, st, *m, *w, c, io, (const double2*)b->K1,
+                           (const double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
+                           b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
+                           all, b->Bp, b->N);
     }
-    if (a->max_ls > 1) {
-        {
-            TimedLaunch tl(b->timing, 2, st);
-            const int gc = grid_for(b->B * (int64_t)(a->max_ls - 1), BLK, 4096);
-            hipLaunchKernelGGL(k_nt_candidates, dim3(gc), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs, b->x_ref,
-                               b->u_ref, b->cost, b->dJ, b->retry_list, b->counters, b->cand_ok, b->Bp, b->N);
-        }
-        TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(k_nt_retry, dim3(grid_for(b->B, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, x, u, K1, cs,
-                           b->x_ref, b->u_ref, xn, un, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf,
-                           b->n_roll, b->retry_list, b->counters, b->cand_ok, hc, b->Bp, b->N);
+    launch_post_trial(m, w, a, b, c, io, all, b->counters, b->stats, nullptr, nullptr, st);
+    return launch_status();
+}
+
+int gym_newton_pipeline_split(const gym_batch* b, int64_t* Bh) {
+    if (!b || !Bh || b->B <= 0) return GYM_EINVAL;
+    int64_t h = ((b->B + 1) / 2 + 63) / 64 * 64;
+    *Bh = h < b->B ? h : b->B;
+    return 0;
+}
+
+int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t p,
+                     int32_t do_backward, void* s) {
+    if (bad_iter_args(m, w, a, b) || p < 0) return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
+    int64_t Bh;
+    gym_newton_pipeline_split(b, &Bh);
+    const Range half[2] = {{0, Bh}, {Bh, b->B}};
+    const bool hist = a->record_history != 0;
+    // backward half: H0 on even phases (iteration p/2), H1 on odd phases (iteration (p-1)/2)
+    const int hb = p & 1, kb = p >> 1;
+    const Range rb = do_backward ? half[hb] : Range{0, 0};
+    // trial half: H0 on odd phases (iteration (p-1)/2), H1 on even phases >= 2 (iteration (p-2)/2)
+    const int ht = (p & 1) ? 0 : 1;
+    const int kt = (p & 1) ? (p - 1) >> 1 : (p - 2) >> 1;
+    const Range rt = (p >= 1) ? half[ht] : Range{0, 0};
+    const int nb_b = (int)((rb.hi - rb.lo + BLK - 1) / BLK), nb_t = (int)((rt.hi - rt.lo + BLK - 1) / BLK);
+    const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, kt < 0 ? 0 : kt, b->hist_len, 0};
+    const TrialIO io = trial_io(b, kt < 0 ? 0 : kt);
+    if (nb_b + nb_t > 0) {
+        TimedLaunch tl(b->timing, (p & 1) ? 5 : 6, st);
+        hipLaunchKernelGGL(k_nt_phase, dim3(nb_b + nb_t), dim3(BLK), 0, st, *m, *w, c, io,
+                           (const double2*)b->x[kb & 1], b->u[kb & 1], kb, nb_b, rb, rt, (double2*)b->K1,
+                           (double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
+                           b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters + ht,
+                           hist ? b->hist_cost : nullptr, hist ? b->hist_smax : nullptr, b->Bp, b->N);
     }
-    TimedLaunch tl(b->timing, 4, st);
-    hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
-                       b->n_iter, b->n_roll, b->partials, b->B, k);
-    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64), 0, st, b->partials, b->counters, b->stats, STAT_BLOCKS);
+    if (p >= 1)  // the trial half's retries and statistics; H1 closes the iteration: total = H0 + H1
+        launch_post_trial(m, w, a, b, c, io, rt, b->counters + ht, b->stats + 8 + 8 * ht,
+                          ht ? b->stats + 8 : nullptr, ht ? b->stats : nullptr, st);
     return launch_status();
 }
 

@@ -11,6 +11,11 @@ The batch runs every lane in lock-step on the device.  Trial 1 is fused with its
 that reject it evaluate trials 2..max_ls *in parallel* (one thread per candidate) and re-run the
 first accepted one -- the same decision the sequential search makes.
 
+Schedules: ``serial`` launches the backward sweep and the trial of all lanes one after the other
+(gym_newton_iteration); ``pipelined`` splits the lanes into two halves offset by one phase and runs
+one half's (HBM-bound) sweep beside the other half's (fp64-VALU-bound) trial in a single launch
+(gym_newton_phase).  Per lane the arithmetic is identical; only the overlap differs.
+
 Multi-GPU: one process per GPU, each owning a contiguous shard of lanes; the only cross-GPU
 traffic is one all-reduce (SUM) of the 8 per-iteration statistics (see distributed.py).
 """
@@ -52,8 +57,10 @@ class SolveResult:
 class BatchedNewtonSolver:
     """Owns the device buffers of a batch of ``B`` lanes that share x_ref / u_ref."""
 
+    PIPELINE_MIN_LANES = 8192
+
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
-                 max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0):
+                 max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         self.eng = engine
@@ -79,7 +86,9 @@ class BatchedNewtonSolver:
         self.counters = torch.zeros(4, dtype=i32, device=dev)
         self.cand_ok = torch.zeros((max(int(max_ls), 1), Bp), dtype=torch.uint8, device=dev)
         self.partials = e(256 * 8)
-        self.stats = torch.zeros(8, dtype=F64, device=dev)
+        self.stats = torch.zeros(24, dtype=F64, device=dev)     # [0,8) totals, [8,16) / [16,24) halves
+        self.pipeline = (self.B >= self.PIPELINE_MIN_LANES) if pipeline is None else bool(pipeline)
+        self.max_iters = None
         self.hist_len = int(hist_len)
         self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
         self.hist_smax = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
@@ -109,7 +118,7 @@ class BatchedNewtonSolver:
 
     def reset_timing(self):
         if self.timing is not None:
-            for i in range(5):
+            for i in range(len(_lib.KERNEL_KINDS)):
                 self.timing.ms[i] = 0.0
                 self.timing.launches[i] = 0
             self.timing.pending = 0
@@ -142,13 +151,27 @@ class BatchedNewtonSolver:
         _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
+        if self.pipeline and (self.max_iters is None or self.max_iters > 0):
+            self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
+
+    def _phase(self, p: int, do_backward: bool):
+        _lib.check(self.eng.lib.gym_newton_phase(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
+                                                 C.byref(self.batch), p, int(do_backward), self.eng.stream),
+                   "gym_newton_phase")
 
     def iteration(self) -> torch.Tensor:
-        _lib.check(self.eng.lib.gym_newton_iteration(C.byref(self.eng.model), C.byref(self.eng._w),
-                                                     C.byref(self.armijo), C.byref(self.batch), self.k,
-                                                     self.eng.stream), "gym_newton_iteration")
+        """Enqueue outer iteration k for every active lane; returns the 8 total statistics (device)."""
+        k = self.k
+        if self.pipeline:
+            more = self.max_iters is None or k + 1 < self.max_iters
+            self._phase(2 * k + 1, True)         # sweep H1 (iteration k) beside trial H0 (iteration k)
+            self._phase(2 * k + 2, more)         # sweep H0 (iteration k+1) beside trial H1 (iteration k)
+        else:
+            _lib.check(self.eng.lib.gym_newton_iteration(C.byref(self.eng.model), C.byref(self.eng._w),
+                                                         C.byref(self.armijo), C.byref(self.batch), k,
+                                                         self.eng.stream), "gym_newton_iteration")
         self.k += 1
-        return self.stats
+        return self.stats[:8]
 
     def finalize(self):
         B, N, T, dev = self.B, self.N, self.T, self.eng.device
@@ -174,6 +197,7 @@ class BatchedNewtonSolver:
         """Run until every lane (of every rank, if ``reduce_stats`` all-reduces) is done or max_iters."""
         torch.cuda.synchronize(self.eng.device)
         t0 = time.perf_counter()
+        self.max_iters = int(max_iters)
         self.init(x0)
         log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every, log_every=log_every,
                           keep_stats=keep_stats)
@@ -220,10 +244,10 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
 
 def newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                        max_ls=MAX_LINE_SEARCH_ITERS, engine: AcrobotEngine | None = None, hist_len=0,
-                       reduce_stats=None) -> SolveResult:
+                       reduce_stats=None, pipeline: bool | None = None) -> SolveResult:
     """Batched newton_Algorithm: x0 (B,4) -> SolveResult (device tensors)."""
     eng = engine or AcrobotEngine()
     x0 = eng.t(x0).reshape(-1, 4)
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, x0.shape[0], tol=tol, beta=beta, c=c, gamma_0=gamma_0,
-                                 max_ls=max_ls, hist_len=hist_len)
+                                 max_ls=max_ls, hist_len=hist_len, pipeline=pipeline)
     return solver.solve(x0, max_iters, reduce_stats=reduce_stats)

@@ -196,7 +196,7 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
                          f"{u_ref.shape[0]} controls (expected {x_ref.shape[0]-1})")
     eng = _eng()
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, 1, tol=tol, beta=beta, c=c, gamma_0=gamma_0,
-                                 max_ls=MAX_LINE_SEARCH_ITERS)
+                                 max_ls=MAX_LINE_SEARCH_ITERS, pipeline=False)
     x0 = np.asarray(x0, dtype=float).reshape(1, 4)
     solver.init(x0)
     Tn = x_ref.shape[0] - 1

@@ -70,10 +70,11 @@ typedef struct gym_armijo {
     int32_t record_history;
 } gym_armijo;
 
-/* Optional per-kernel timing of gym_newton_iteration with HIP events on the solver's stream.
- * Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
- * rollout, 4 statistics.  A pair is recorded only if the previous one was collected. */
-#define GYM_NK 5
+/* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
+ * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
+ * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p).  A pair is recorded only if the
+ * previous one of its kind was collected. */
+#define GYM_NK 7
 typedef struct gym_timing {
     void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
     double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
@@ -101,10 +102,10 @@ typedef struct gym_batch {
     int32_t* res_buf;   /* (Bp) which x/u buffer holds a finished lane's result   */
     int32_t* n_roll;    /* (Bp) closed-loop rollouts evaluated                     */
     int32_t* retry_list;/* (Bp) lanes that need Armijo trials 2..max_ls           */
-    int32_t* counters;  /* (4)  [0] = retry count                                 */
+    int32_t* counters;  /* (4)  retry counts: [0] serial schedule / half H0, [1] half H1 */
     uint8_t* cand_ok;   /* (max_ls, Bp) Armijo acceptance of candidate j           */
     double* partials;   /* (256*8) per-block statistics                           */
-    double* stats;      /* (8) see gym_newton_iteration                           */
+    double* stats;      /* (24) [0,8) totals (see gym_newton_iteration), [8,16) H0, [16,24) H1 */
     double* hist_cost;  /* optional (hist_len, Bp): J after iteration k            */
     double* hist_smax;  /* optional (hist_len, Bp): max|sigma| of iteration k      */
     gym_timing* timing; /* [host] optional kernel timing (NULL: none)               */
@@ -180,6 +181,16 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
  * Buffer roles: x/u[k&1] = current, x/u[(k+1)&1] = candidate.  Stream-ordered, no host sync. */
 int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt,
                          int32_t k, void* stream);
+/* Pipelined schedule: lanes split into halves H0 = [0, Bh), H1 = [Bh, B) (gym_newton_pipeline_split) whose
+ * iterations are offset by one phase.  Phase p runs ONE fused launch: the backward sweep of H0 (p even,
+ * iteration p/2) or H1 (p odd, iteration (p-1)/2) -- skipped if do_backward == 0, i.e. past max_iters --
+ * beside the Armijo trial of the other half (H0 for odd p, iteration (p-1)/2; H1 for even p >= 2,
+ * iteration (p-2)/2); then that half's candidate trials, retries and statistics.  After phase 2k+2 both
+ * halves have completed iteration k and stats[0,8) holds the totals.  Call p = 0 once after init; every
+ * lane follows exactly the serial schedule's arithmetic. */
+int gym_newton_pipeline_split(const gym_batch* bt, int64_t* Bh);
+int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t p,
+                     int32_t do_backward, void* stream);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
  * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
  * (sigma0 recomputed from that iteration's u0).  Any output may be NULL. */

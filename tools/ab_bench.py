@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of library variants in ONE process on one device (measurement tool).
 
-    python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so ...
+    python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so:serial lib_b.so:pipe ...
+(a ":serial" / ":pipe" suffix selects the schedule; default: the solver's choice)
 Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
 kernel library is swapped), so buffer placement -- worth +-4% on its own -- is held fixed; prints
 per-variant median backward / trial kernel times and whole-solve throughput.
@@ -31,21 +32,31 @@ def main():
     x_ref, u_ref = load_refs()
     x0 = make_x0(a.batch)
     from gymnast_optimalcontrol_amd import _lib
-    eng = AcrobotEngine(lib_path=os.path.abspath(a.libs[0]))
+    def split(spec):
+        path, _, sched = spec.partition(":")
+        return os.path.abspath(path), {"serial": False, "pipe": True}.get(sched)
+    eng = AcrobotEngine(lib_path=split(a.libs[0])[0])
     s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1).enable_timing()
+    default_pipe = s.pipeline
     xd = eng.t(x0)
-    libs = {p: _lib.load(os.path.abspath(p)) for p in a.libs}
+    libs = {p: _lib.load(split(p)[0]) for p in a.libs}
     res = {p: {"bwd": [], "trial": [], "its": [], "sec": []} for p in a.libs}
     for r in range(a.rounds + 1):
         for p in a.libs:
             eng.lib = libs[p]
+            sched = split(p)[1]
+            s.pipeline = default_pipe if sched is None else sched
             s.reset_timing()
             out = s.solve(xd, a.max_iters)
             kt = s.kernel_times()
             if r == 0:
                 continue   # warm-up round
-            res[p]["bwd"].append(kt["backward"][0] / kt["backward"][1])
-            res[p]["trial"].append(kt["trial"][0] / kt["trial"][1])
+            if kt["backward"][1]:
+                res[p]["bwd"].append(kt["backward"][0] / kt["backward"][1])
+                res[p]["trial"].append(kt["trial"][0] / kt["trial"][1])
+            else:   # pipelined: report the phase pair as "bwd" (odd) / "trial" (even)
+                res[p]["bwd"].append(kt["phase_odd"][0] / max(1, kt["phase_odd"][1]))
+                res[p]["trial"].append(kt["phase_even"][0] / max(1, kt["phase_even"][1]))
             res[p]["its"].append(out.lane_iterations / out.seconds)
             res[p]["sec"].append(out.seconds)
     for p in a.libs:
