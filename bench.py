@@ -33,18 +33,22 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
 
 
-def algorithmic_bytes(N: int) -> dict:
+def algorithmic_bytes(N: int, u0_zero: bool = True) -> dict:
     """Compulsory HBM bytes per lane for one pass of each solver kernel (fp64), see DESIGN.md section 4.
 
     backward sweep : read x (4N) + u (2T);            write K row 1 (4T) + (c1, sigma1) (2T)
     Armijo trial   : read K row 1 (4T) + (c1, sigma1) (2T) + u0 (T) + x_0 (4);
                      write x_new (4N) + u_new (2T)
-    A Newton iteration of one lane is one sweep + one trial (no backtracking) = 100,096 B at N = 501.
-    (SURVEY.md 8(d)'s 152,096 B is the reference's data flow: K stored 2x4 and the trial re-reading x, u.)
+    u0_zero (u_ref[:,0] == 0, GYM_FLAG_U0_ZERO): the tau1 plane is neither read nor written (-T on
+    the sweep's reads, -T / -T on the trial's reads / writes).
+    A Newton iteration of one lane is one sweep + one trial (no backtracking): 100,096 B at N = 501,
+    88,096 B with u0_zero.  (SURVEY.md 8(d)'s 152,096 B is the reference's data flow: K stored 2x4,
+    sigma stored 2-wide and the trial re-reading x and u.)
     """
     T = N - 1
-    bwd = 8 * (4 * N + 2 * T + 4 * T + 2 * T)
-    trial = 8 * (4 * T + 2 * T + T + 4 + 4 * N + 2 * T)
+    z = T if u0_zero else 0
+    bwd = 8 * (4 * N + 2 * T - z + 4 * T + 2 * T)
+    trial = 8 * (4 * T + 2 * T + (T - z) + 4 + 4 * N + 2 * T - z)
     return {"backward": bwd, "trial": trial, "iteration": bwd + trial,
             "survey_per_iteration": 8 * ((4 * N + 2 * T) + 10 * T + (2 * (4 * N + 2 * T) + 10 * T))}
 
@@ -89,6 +93,11 @@ def main():
     ap.add_argument("--cpu-lanes", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--sync-every", type=int, default=4,
+                    help="outer iterations between host reads of the (all-reduced) statistics; iterations "
+                         "enqueued after every lane has finished are no-ops")
+    ap.add_argument("--schedule", choices=("auto", "serial", "pipelined"), default="auto",
+                    help="solver schedule (auto: the solver's choice for the batch size)")
     a = ap.parse_args()
 
     import torch
@@ -107,14 +116,15 @@ def main():
     x0_all = make_x0(total)
     lo, hi = gd.shard_range(total, rank, world)
     eng = AcrobotEngine()
-    solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20)
+    solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20,
+                                 pipeline={"auto": None, "serial": False, "pipelined": True}[a.schedule])
     if not a.no_timing:
         solver.enable_timing()
     x0_dev = eng.t(x0_all[lo:hi])                  # inputs resident in HBM before the timed region
     reduce = gd.make_reduce_stats()
 
     for _ in range(a.warmup):
-        solver.solve(x0_dev, a.max_iters, reduce_stats=reduce)
+        solver.solve(x0_dev, a.max_iters, reduce_stats=reduce, sync_every=a.sync_every)
     solver.reset_timing()
     gd.barrier()
     torch.cuda.synchronize()
@@ -122,7 +132,7 @@ def main():
     lane_its = 0
     res = None
     for _ in range(a.steps):
-        res = solver.solve(x0_dev, a.max_iters, reduce_stats=reduce)
+        res = solver.solve(x0_dev, a.max_iters, reduce_stats=reduce, sync_every=a.sync_every)
         lane_its += res.lane_iterations
     torch.cuda.synchronize()
     gd.barrier()
@@ -156,7 +166,7 @@ def main():
            "states_per_s": value * T}
 
     if kt and rank == 0:
-        ab = algorithmic_bytes(N)
+        ab = algorithmic_bytes(N, solver.u0_zero)
         kern = {}
         for kind, (ms, launches) in kt.items():
             if launches:
@@ -195,7 +205,9 @@ def main():
                            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 PMC, 20-iteration run, all lanes "
                                              "active)", "bytes_per_unit": bytes_per_lane,
                            "unit_of_work": unit_note, "algorithmic_bytes_per_launch":
-                           kern[dom]["algorithmic_bytes_per_launch"]}
+                           kern[dom]["algorithmic_bytes_per_launch"], "u0_zero_streams_skipped": solver.u0_zero,
+                           "survey_bytes_per_iteration": ab["survey_per_iteration"],
+                           "whole_solve_GBs_at_survey_bytes": value * ab["survey_per_iteration"] / 1e9 / world}
         out["kernels"] = kern
         out["schedule"] = "pipelined" if solver.pipeline else "serial"
     if parity is not None:

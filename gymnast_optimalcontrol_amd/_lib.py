@@ -12,7 +12,8 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 from . import _build
 
-LIB_PATH = _build.LIB_PATH
+# GYM_LIB_PATH selects another build of the same library (measurement / diagnostic variants)
+LIB_PATH = os.environ.get("GYM_LIB_PATH") or _build.LIB_PATH
 
 # exported symbols, in include/gymnast_acrobot.h order (tests check every one is present)
 EXPORTS = (
@@ -26,6 +27,10 @@ EXPORTS = (
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even")
+
+ABI_VERSION = 2          # GYM_ABI_VERSION of the header this binding mirrors
+MAX_BP = 1 << 26         # GYM_MAX_BP
+FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4
 STATUS_NAMES = {ACTIVE: "active", CONVERGED: "converged", LS_FAILED: "ls_failed", MAX_ITERS: "max_iters", PAD: "pad"}
@@ -54,7 +59,7 @@ class GymTiming(C.Structure):
 
 class GymBatch(C.Structure):
     _fields_ = [("B", C.c_int64), ("Bp", C.c_int64), ("N", C.c_int32), ("hist_len", C.c_int32),
-                ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("cs", _P), ("x_ref", _P), ("u_ref", _P),
+                ("flags", C.c_int32), ("pad", C.c_int32), ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("cs", _P), ("x_ref", _P), ("u_ref", _P),
                 ("cost", _P), ("dJ", _P), ("smax", _P), ("gamma", _P), ("status", _P), ("n_iter", _P),
                 ("res_buf", _P), ("n_roll", _P), ("retry_list", _P), ("counters", _P), ("cand_ok", _P),
                 ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P),
@@ -101,6 +106,10 @@ def load(path: str = LIB_PATH):
                 f"{path} is missing: build the HIP library first (python -m gymnast_optimalcontrol_amd._build "
                 "or __graft_entry__.build()); there is no CPU fallback")
         lib = C.CDLL(path)
+        lib.gym_abi_version.restype = C.c_int
+        if lib.gym_abi_version() != ABI_VERSION:
+            raise ImportError(f"{path} implements ABI {lib.gym_abi_version()}, this binding needs {ABI_VERSION}: "
+                              "rebuild the HIP library")
         for name, args in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = args

@@ -101,25 +101,34 @@ __device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, dou
     q2 = (M11 * r2 - M12 * r1) * inv;
 }
 
-// sin/cos of th + d from sin/cos of th (angle addition; d is an RK4 sub-step displacement, so
-// |d| <= pi/4 unless |w| > 39 rad/s, in which case the argument is reduced from scratch).
-#ifndef GYM_RK4_ROTATE
-#define GYM_RK4_ROTATE 0
-#endif
-__device__ __forceinline__ void rotate(double th, double d, double s, double c, double& so, double& co) {
-    if (GYM_RK4_ROTATE && __builtin_expect(fabs(d) <= 0.78539816339744830962, 1)) {
-        const double z = d * d;
-        const double sd = ksin(d, z), cd = kcos(z);
-        so = fma(s, cd, c * sd);
-        co = fma(c, cd, -(s * sd));
-    } else {
-        fast_sincos(th + d, &so, &co);
+// sin/cos of the RK4 sub-step angles (th1 + d1, th2 + d2) from those of the step's base angles by angle
+// addition: cos/sin(d) from the minimax kernels (no argument reduction, no quadrant logic) plus a
+// rotation, ~20 VALU instead of ~40 for a reduction from scratch.  d = (h/2) w or h w is small; a lane
+// with |d| > pi/4 (|w| > 39 rad/s) reduces both arguments from scratch instead.  The choice is per lane,
+// so a lane's arithmetic never depends on which other lanes share its wavefront.
+__device__ __forceinline__ void rotate(double s, double c, double d, double& so, double& co) {
+    const double z = d * d;
+    const double sd = ksin(d, z), cd = kcos(z);
+    so = fma(s, cd, c * sd);
+    co = fma(c, cd, -(s * sd));
+}
+
+__device__ __forceinline__ void substep_sincos(double th1, double th2, double d1, double d2, double s1, double c1,
+                                               double s2, double c2, double& t1, double& u1, double& t2,
+                                               double& u2) {
+    constexpr double kPio4 = 0.78539816339744830962;
+    if (__builtin_expect(fabs(d1) <= kPio4 && fabs(d2) <= kPio4, 1)) {
+        rotate(s1, c1, d1, t1, u1);
+        rotate(s2, c2, d2, t2, u2);
+    } else {   // also taken by NaN lanes
+        fast_sincos(th1 + d1, &t1, &u1);
+        fast_sincos(th2 + d2, &t2, &u2);
     }
 }
 
-// Classic RK4 with the control held over the step (dynamics.py:177-195), in place.  The angles of
-// the three sub-step states are x + d with d = (h/2) k1, (h/2) k2, h k3; their sin/cos come from
-// angle addition on the step's base angles, so only the base angles need an argument reduction.
+// Classic RK4 with the control held over the step (dynamics.py:177-195), in place.  Only the step's
+// base angles are reduced from scratch; the three sub-step states' angles x + d, d = (h/2) k1, (h/2) k2,
+// h k3, get their sin/cos by angle addition (substep_sincos).
 __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2) {
     double a1, b1, a2, b2, a3, b3, a4, b4;
     double s1, c1, s2, c2, t1, u1, t2, u2;
@@ -127,16 +136,13 @@ __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double
     fast_sincos(x1, &s2, &c2);
     accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
     const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
-    rotate(x0, m.h2 * x2, s1, c1, t1, u1);
-    rotate(x1, m.h2 * x3, s2, c2, t2, u2);
+    substep_sincos(x0, x1, m.h2 * x2, m.h2 * x3, s1, c1, s2, c2, t1, u1, t2, u2);
     accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
     const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
-    rotate(x0, m.h2 * y2, s1, c1, t1, u1);
-    rotate(x1, m.h2 * y3, s2, c2, t2, u2);
+    substep_sincos(x0, x1, m.h2 * y2, m.h2 * y3, s1, c1, s2, c2, t1, u1, t2, u2);
     accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
     const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
-    rotate(x0, m.h * z2, s1, c1, t1, u1);
-    rotate(x1, m.h * z3, s2, c2, t2, u2);
+    substep_sincos(x0, x1, m.h * z2, m.h * z3, s1, c1, s2, c2, t1, u1, t2, u2);
     accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
     const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
     const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;

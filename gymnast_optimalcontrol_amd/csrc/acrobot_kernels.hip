@@ -53,6 +53,37 @@ __device__ __forceinline__ void st_nt(double2* p, double a, double b) {
 }
 __device__ __forceinline__ void st_nt(double* p, double a) { __builtin_nontemporal_store(a, p); }
 
+// Completes the prefetch loads of the first stage before a software-pipelined stage loop is entered
+// (an empty asm that reads the registers forces the wait here, in the preheader).  Without it the loop
+// header merges the preheader's pending loads with the back edge's pending stores, and the compiler
+// then waits for every store of the previous stage at the top of each iteration, i.e. one full HBM
+// write round trip per stage.
+// Solver streams through buffer instructions: the stage row's base address lives in a wave-uniform
+// buffer resource (SGPRs, rebased per stage by scalar adds), the lane's byte offset in one 32-bit VGPR
+// and the row-within-stage offset in an SGPR.  Compared with 64-bit per-lane pointers this frees ~14
+// VGPRs and the per-stage 64-bit address arithmetic.  Offsets stay below 2^31 (Bp <= GYM_MAX_BP).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kNT = 2;  // gfx950 cache-policy bits: nt (streamed once)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, kNT));
+}
+__device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, kNT));
+}
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a, double b) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, kNT);
+}
+__device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, kNT);
+}
+
+__device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
+__device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "v"(v.y)); }
+
 // element index of (t, component-group p of P, lane) in a time-major SoA stream
 __device__ __forceinline__ int64_t pix(int t, int p, int P, int64_t l, int64_t Bp) { return ((int64_t)t * P + p) * Bp + l; }
 
@@ -111,7 +142,13 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const gym_weights& w
 //   u_new1 = (c1 + K1 x_new) + gamma sigma1,  c1 = u1 - K1 x  (the sweep's offset)
 // Streams per stage: K1 (2 pairs) + (c1, sigma1) (1 pair) + u0 (plane) in; x_new, u_new out.
 // ------------------------------------------------------------------------------------------
-template <bool WRITE>
+// Streams of one stage of the offset-form rollout, prefetched into registers one stage ahead.
+struct TrialStage {
+    double2 k0, k1, c;   // K row 1 (two pairs), (c1, sigma1)
+    double u0;           // tau1 control (0 when U0Z)
+};
+
+template <bool WRITE, bool U0Z>
 __device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights& w, const double* __restrict__ u,
                                                 const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                 const double* __restrict__ xr, const double* __restrict__ ur,
@@ -120,40 +157,51 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights&
                                                 double n3) {
     const int T = N - 1;
     const double G00 = 2.0 * w.R[0], iG00 = 1.0 / G00;
+    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;   // lane byte offsets (pairs, planes)
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(K1);   // stage stride 2 rows
+    const char* Cb = reinterpret_cast<const char*>(cs);   // stage stride 1 row
+    const char* Ub = reinterpret_cast<const char*>(u);    // stage stride 2 planes = 1 row
+    const char* Xb = reinterpret_cast<const char*>(xn);   // stage stride 2 rows
+    const char* Ob = reinterpret_cast<const char*>(un);   // stage stride 1 row
     double J = 0.0;
     if (WRITE) {
-        st_nt(&xn[l], n0, n1);
-        st_nt(&xn[Bp + l], n2, n3);
+        const auto rX = rsrc(Xb);
+        bst2(rX, o2, 0, n0, n1);
+        bst2(rX, o2, row, n2, n3);
     }
-    // software prefetch of stage t+1's streams while stage t computes
-    double2 pk0 = ld_nt(&K1[pix(0, 0, 2, l, Bp)]), pk1 = ld_nt(&K1[pix(0, 1, 2, l, Bp)]);
-    double2 pc = ld_nt(&cs[l]);
-    double pu0 = ld_nt(&u[l]);
+    auto fetch = [&](TrialStage& q, int t) {   // stage t's streams into register set q
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        q.k0 = bld2(rK, o2, 0);
+        q.k1 = bld2(rK, o2, row);
+        q.c = bld2(rsrc(Cb + (int64_t)t * row), o2, 0);
+        q.u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
+    };
+    TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
+    fetch(pre, 0);
+    pin(pre.k0); pin(pre.k1); pin(pre.c); pin(pre.u0);
     for (int t = 0; t < T; ++t) {
-        const double2 k0 = pk0, k1 = pk1, c = pc;
-        const double u0 = pu0;
-        if (t + 1 < T) {
-            pk0 = ld_nt(&K1[pix(t + 1, 0, 2, l, Bp)]);
-            pk1 = ld_nt(&K1[pix(t + 1, 1, 2, l, Bp)]);
-            pc = ld_nt(&cs[(int64_t)(t + 1) * Bp + l]);
-            pu0 = ld_nt(&u[pix(t + 1, 0, 2, l, Bp)]);
-        }
+        const double2 k0 = pre.k0, k1 = pre.k1, c = pre.c;
+        const double u0 = pre.u0;
+        if (t + 1 < T) fetch(pre, t + 1);
         const double* urt = ur + 2 * t;
         const double s0 = -(G00 * (u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
-        const double v0 = u0 + gamma * s0;
+        const double v0 = u0 + gamma * s0;                 // U0Z: u0 = ur0 = 0  =>  v0 = +0 exactly
         const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
         const double v1 = (c.x + kx) + gamma * c.y;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
         J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
         J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
         if (WRITE) {
-            st_nt(&un[pix(t, 0, 2, l, Bp)], v0);
-            st_nt(&un[pix(t, 1, 2, l, Bp)], v1);
+            const auto rO = rsrc(Ob + (int64_t)t * row);
+            if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
+            bst1(rO, o1, plane, v1);
         }
         gym::rk4(m, n0, n1, n2, n3, v1);
         if (WRITE) {
-            st_nt(&xn[pix(t + 1, 0, 2, l, Bp)], n0, n1);
-            st_nt(&xn[pix(t + 1, 1, 2, l, Bp)], n2, n3);
+            const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
+            bst2(rX, o2, 0, n0, n1);
+            bst2(rX, o2, row, n2, n3);
         }
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
@@ -165,53 +213,35 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights&
 //   A_d = I + dt A_c with A_c rows 0,1 = e3^T, e4^T ; B_d = dt B_c with only column 1 non-zero
 //   Q_t = 2Q, R_t = 2R (diagonal), S_t = 0  =>  G = diag(2R0, 2R1 + b^T P b), K_t row 0 = 0.
 // P is kept symmetric (10 registers), p and (optionally) the costate lambda in registers.
-// SOLVER: writes K1 and (c1 = u1 - K1 x, sigma1); API: writes K1 and sigma planes (+ lambda).
 // ------------------------------------------------------------------------------------------
-template <bool SOLVER, bool LAMBDA>
-__device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
-                                              const double* __restrict__ u, const double* __restrict__ xr,
-                                              const double* __restrict__ ur, double2* __restrict__ K1,
-                                              double2* __restrict__ cs, double* __restrict__ sig,
-                                              double2* __restrict__ lam, int64_t l, int64_t Bp, int N,
-                                              double& dJ_out, double& smax_out) {
-    const int T = N - 1;
-    const double dt = m.h;
+template <bool LAMBDA>
+struct Sweep {
     double P00, P01, P02, P03, P11, P12, P13, P22, P23, P33, p0, p1, p2, p3;
     double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-    {
-        const double2 xa = x[pix(T, 0, 2, l, Bp)], xb = x[pix(T, 1, 2, l, Bp)];
-        const double* xrT = xr + 4 * T;
+    double dJ = 0.0, smax = 0.0;
+    double twoQ0, twoQ1, twoQ2, twoQ3, G00, twoR1, iG00;
+
+    // terminal conditions from x_N (P = 2 Q_T, p = 2 Q_T dx_N; lambda_N = p)
+    __device__ __forceinline__ Sweep(const gym_weights& w, double2 xa, double2 xb, const double* xrT) {
         P00 = 2.0 * w.QT[0]; P11 = 2.0 * w.QT[1]; P22 = 2.0 * w.QT[2]; P33 = 2.0 * w.QT[3];
         P01 = P02 = P03 = P12 = P13 = P23 = 0.0;
         p0 = P00 * (xa.x - xrT[0]); p1 = P11 * (xa.y - xrT[1]);
         p2 = P22 * (xb.x - xrT[2]); p3 = P33 * (xb.y - xrT[3]);
-        if (LAMBDA) {
-            l0 = p0; l1 = p1; l2 = p2; l3 = p3;
-            lam[pix(T, 0, 2, l, Bp)] = make_double2(l0, l1);
-            lam[pix(T, 1, 2, l, Bp)] = make_double2(l2, l3);
-        }
+        if (LAMBDA) { l0 = p0; l1 = p1; l2 = p2; l3 = p3; }
+        twoQ0 = 2.0 * w.Q[0]; twoQ1 = 2.0 * w.Q[1]; twoQ2 = 2.0 * w.Q[2]; twoQ3 = 2.0 * w.Q[3];
+        G00 = 2.0 * w.R[0]; twoR1 = 2.0 * w.R[1]; iG00 = 1.0 / G00;
     }
-    const double twoQ0 = 2.0 * w.Q[0], twoQ1 = 2.0 * w.Q[1], twoQ2 = 2.0 * w.Q[2], twoQ3 = 2.0 * w.Q[3];
-    const double G00 = 2.0 * w.R[0], twoR1 = 2.0 * w.R[1], iG00 = 1.0 / G00;
-    double dJ = 0.0, smax = 0.0;
-    double2 pa = ld_nt(&x[pix(T - 1, 0, 2, l, Bp)]), pb = ld_nt(&x[pix(T - 1, 1, 2, l, Bp)]);
-    double pu0 = ld_nt(&u[pix(T - 1, 0, 2, l, Bp)]), pu1 = ld_nt(&u[pix(T - 1, 1, 2, l, Bp)]);
-    for (int t = T - 1; t >= 0; --t) {
-        const double2 xa = pa, xb = pb;
-        const double ut0 = pu0, ut1 = pu1;
-        if (t > 0) {
-            pa = ld_nt(&x[pix(t - 1, 0, 2, l, Bp)]);
-            pb = ld_nt(&x[pix(t - 1, 1, 2, l, Bp)]);
-            pu0 = ld_nt(&u[pix(t - 1, 0, 2, l, Bp)]);
-            pu1 = ld_nt(&u[pix(t - 1, 1, 2, l, Bp)]);
-        }
+
+    // stage t (x_t = (xa, xb), u_t = (ut0, ut1)): gain row 1 k[0..3], sigma (s0, s1); updates P, p, dJ, smax
+    __device__ __forceinline__ void step(const Dyn& m, double2 xa, double2 xb, double ut0, double ut1,
+                                         const double* xrt, const double* urt, double& k0, double& k1,
+                                         double& k2, double& k3, double& s0, double& s1) {
+        const double dt = m.h;
         const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1);
         // A_d rows 2,3 (rows 0,1 = [1 0 dt 0], [0 1 0 dt]); B_d = dt * [0 0 bc2 bc3]^T in column 1
         const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
         const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
         const double bd2 = dt * J.bc2, bd3 = dt * J.bc3;
-        const double* xrt = xr + 4 * t;
-        const double* urt = ur + 2 * t;
         const double q0 = twoQ0 * (xa.x - xrt[0]), q1 = twoQ1 * (xa.y - xrt[1]);
         const double q2 = twoQ2 * (xb.x - xrt[2]), q3 = twoQ3 * (xb.y - xrt[3]);
         const double r0 = G00 * (ut0 - urt[0]), r1 = twoR1 * (ut1 - urt[1]);
@@ -221,8 +251,6 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
             const double n2 = q2 + (dt * l0 + A22 * l2 + A32 * l3);
             const double n3 = q3 + (dt * l1 + A23 * l2 + A33 * l3);
             l0 = n0; l1 = n1; l2 = n2; l3 = n3;
-            lam[pix(t, 0, 2, l, Bp)] = make_double2(l0, l1);
-            lam[pix(t, 1, 2, l, Bp)] = make_double2(l2, l3);
         }
         // Pb = P B_d[:,1]
         const double Pb0 = P02 * bd2 + P03 * bd3, Pb1 = P12 * bd2 + P13 * bd3;
@@ -235,8 +263,8 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         const double F3 = dt * Pb1 + A23 * Pb2 + A33 * Pb3;
         const double g1 = r1 + (bd2 * p2 + bd3 * p3);
         const double iG = 1.0 / G11;
-        const double k0 = -F0 * iG, k1 = -F1 * iG, k2 = -F2 * iG, k3 = -F3 * iG;
-        const double s0 = -r0 * iG00, s1 = -g1 * iG;
+        k0 = -F0 * iG; k1 = -F1 * iG; k2 = -F2 * iG; k3 = -F3 * iG;
+        s0 = -r0 * iG00; s1 = -g1 * iG;
         dJ += r0 * s0 + g1 * s1;
         // W = P A_d
         const double W00 = P00 + P02 * A20 + P03 * A30, W01 = P01 + P02 * A21 + P03 * A31;
@@ -268,21 +296,95 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
         P00 = nP00; P01 = nP01; P02 = nP02; P03 = nP03; P11 = nP11; P12 = nP12; P13 = nP13;
         P22 = nP22; P23 = nP23; P33 = nP33;
         p0 = np0; p1 = np1; p2 = np2; p3 = np3;
-        if (SOLVER) {
-            const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
-            st_nt(&K1[pix(t, 0, 2, l, Bp)], k0, k1);
-            st_nt(&K1[pix(t, 1, 2, l, Bp)], k2, k3);
-            st_nt(&cs[(int64_t)t * Bp + l], c1, s1);
-        } else {
-            K1[pix(t, 0, 2, l, Bp)] = make_double2(k0, k1);
-            K1[pix(t, 1, 2, l, Bp)] = make_double2(k2, k3);
-            sig[pix(t, 0, 2, l, Bp)] = s0;
-            sig[pix(t, 1, 2, l, Bp)] = s1;
-        }
         smax = gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
     }
-    dJ_out = dJ;
-    smax_out = smax;
+};
+
+// API form: writes K row 1 (pairs), sigma planes and optionally lambda; register prefetch of stage t-1.
+template <bool LAMBDA>
+__device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+                                              const double* __restrict__ u, const double* __restrict__ xr,
+                                              const double* __restrict__ ur, double2* __restrict__ K1,
+                                              double* __restrict__ sig, double2* __restrict__ lam, int64_t l,
+                                              int64_t Bp, int N, double& dJ_out, double& smax_out) {
+    const int T = N - 1;
+    Sweep<LAMBDA> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    if (LAMBDA) {
+        lam[pix(T, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
+        lam[pix(T, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
+    }
+    double2 pa = x[pix(T - 1, 0, 2, l, Bp)], pb = x[pix(T - 1, 1, 2, l, Bp)];
+    double pu0 = u[pix(T - 1, 0, 2, l, Bp)], pu1 = u[pix(T - 1, 1, 2, l, Bp)];
+    for (int t = T - 1; t >= 0; --t) {
+        const double2 xa = pa, xb = pb;
+        const double ut0 = pu0, ut1 = pu1;
+        if (t > 0) {
+            pa = x[pix(t - 1, 0, 2, l, Bp)];
+            pb = x[pix(t - 1, 1, 2, l, Bp)];
+            pu0 = u[pix(t - 1, 0, 2, l, Bp)];
+            pu1 = u[pix(t - 1, 1, 2, l, Bp)];
+        }
+        double k0, k1, k2, k3, s0, s1;
+        S.step(m, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        if (LAMBDA) {
+            lam[pix(t, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
+            lam[pix(t, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
+        }
+        K1[pix(t, 0, 2, l, Bp)] = make_double2(k0, k1);
+        K1[pix(t, 1, 2, l, Bp)] = make_double2(k2, k3);
+        sig[pix(t, 0, 2, l, Bp)] = s0;
+        sig[pix(t, 1, 2, l, Bp)] = s1;
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// Solver sweep of one lane: writes K row 1 and (c1 = u1 - K1 x, sigma1), prefetching stage t-1's
+// streams while stage t computes.  U0Z: the tau1 channel is identically zero (u0 = ur0 = 0,
+// GYM_FLAG_U0_ZERO) and its plane is not read.
+template <bool U0Z>
+__device__ __forceinline__ void backward_solver_lane(const Dyn& m, const gym_weights& w,
+                                                     const double2* __restrict__ x, const double* __restrict__ u,
+                                                     const double* __restrict__ xr, const double* __restrict__ ur,
+                                                     double2* __restrict__ K1, double2* __restrict__ cs, int64_t l,
+                                                     int64_t Bp, int N, double& dJ_out, double& smax_out) {
+    const int T = N - 1;
+    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;   // lane byte offsets (pairs, planes)
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Xb = reinterpret_cast<const char*>(x);    // stage stride 2 rows
+    const char* Ub = reinterpret_cast<const char*>(u);    // stage stride 1 row
+    const char* Kb = reinterpret_cast<const char*>(K1);
+    const char* Cb = reinterpret_cast<const char*>(cs);
+    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    double2 pa, pb;
+    double pu0 = 0.0, pu1;
+    {
+        const auto rX = rsrc(Xb + (int64_t)(T - 1) * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)(T - 1) * row);
+        pa = bld2(rX, o2, 0); pb = bld2(rX, o2, row); pu1 = bld1(rU, o1, plane);
+        if (!U0Z) pu0 = bld1(rU, o1, 0);
+    }
+    pin(pa); pin(pb); pin(pu0); pin(pu1);
+    for (int t = T - 1; t >= 0; --t) {
+        const double2 xa = pa, xb = pb;
+        const double ut0 = pu0, ut1 = pu1;
+        if (t > 0) {
+            const auto rX = rsrc(Xb + (int64_t)(t - 1) * (2 * (int64_t)row));
+            const auto rU = rsrc(Ub + (int64_t)(t - 1) * row);
+            pa = bld2(rX, o2, 0);
+            pb = bld2(rX, o2, row);
+            if (!U0Z) pu0 = bld1(rU, o1, 0);
+            pu1 = bld1(rU, o1, plane);
+        }
+        double k0, k1, k2, k3, s0, s1;
+        S.step(m, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        bst2(rK, o2, 0, k0, k1);
+        bst2(rK, o2, row, k2, k3);
+        bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -299,9 +401,9 @@ __global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights 
     const Dyn m(mm);
     double d, s;
     if (lam)
-        backward_lane<false, true>(m, w, x, u, xr, ur, K1, nullptr, sig, lam, l, Bp, N, d, s);
+        backward_lane<true>(m, w, x, u, xr, ur, K1, sig, lam, l, Bp, N, d, s);
     else
-        backward_lane<false, false>(m, w, x, u, xr, ur, K1, nullptr, sig, nullptr, l, Bp, N, d, s);
+        backward_lane<false>(m, w, x, u, xr, ur, K1, sig, nullptr, l, Bp, N, d, s);
     if (dJ) dJ[l] = d;
     if (smax) smax[l] = s;
 }
@@ -654,12 +756,36 @@ __global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const
                                  x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
 }
 
+// Diagnostic build only (-DGYM_WAVE_TRACE, tools/wave_trace.py): per-wavefront start/end time and
+// hardware placement of the serial schedule's sweep (kind 0) and trial (kind 1) launches.
+#ifdef GYM_WAVE_TRACE
+__device__ unsigned long long g_wave_trace[2][8192][4];
+struct WaveTrace {
+    int kind;
+    unsigned long long t0;
+    __device__ explicit WaveTrace(int k) : kind(k), t0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~WaveTrace() {
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {
+            unsigned long long* r = g_wave_trace[kind][blockIdx.x];
+            r[0] = t0;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+            r[3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+        }
+    }
+};
+#define GYM_TRACE_WAVE(k) WaveTrace wave_trace_(k)
+#else
+#define GYM_TRACE_WAVE(k)
+#endif
+
 // Lane ranges: the serial schedule runs every lane [0, B); the pipelined schedule splits the batch
 // into two halves H0 = [0, Bh), H1 = [Bh, B) whose iterations are offset by one phase.
 struct Range {
     int64_t lo, hi;
 };
 
+template <bool U0Z>
 __device__ __forceinline__ void backward_solver(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
                                                 const double* __restrict__ u, const double* __restrict__ xr,
                                                 const double* __restrict__ ur, double2* __restrict__ K1,
@@ -667,12 +793,13 @@ __device__ __forceinline__ void backward_solver(const Dyn& m, const gym_weights&
                                                 double* __restrict__ smax, double* __restrict__ hist_smax, int64_t l,
                                                 int64_t Bp, int N, int k, int hist_len) {
     double d, s;
-    backward_lane<true, false>(m, w, x, u, xr, ur, K1, cs, nullptr, nullptr, l, Bp, N, d, s);
+    backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
 }
 
+template <bool U0Z>
 __global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weights w, const double2* __restrict__ x,
                                                         const double* __restrict__ u, const double* __restrict__ xr,
                                                         const double* __restrict__ ur, double2* __restrict__ K1,
@@ -681,10 +808,11 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weight
                                                         const int32_t* __restrict__ status,
                                                         double* __restrict__ hist_smax, Range rg, int64_t Bp, int N,
                                                         int k, int hist_len) {
+    GYM_TRACE_WAVE(0);
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
     const Dyn m(mm);
-    backward_solver(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len);
+    backward_solver<U0Z>(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len);
 }
 
 struct SolverCtl {
@@ -718,6 +846,7 @@ struct TrialIO {
 };
 
 // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass).
+template <bool U0Z>
 __device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w, const SolverCtl& a, const TrialIO& io,
                                              const double2* __restrict__ K1, const double2* __restrict__ cs,
                                              const double* __restrict__ xr, const double* __restrict__ ur,
@@ -729,8 +858,8 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w,
                                              double* __restrict__ hist_cost, int64_t l, int64_t Bp, int N) {
     const double2 xa = io.x[l], xb = io.x[Bp + l];
     const double g = a.gamma0;
-    const double Jn = rollout_cform<true>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y, xb.x,
-                                          xb.y);
+    const double Jn = rollout_cform<true, U0Z>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y,
+                                               xb.x, xb.y);
     n_roll[l] += 1;
     if (Jn < cost[l] + a.c * g * dJ[l]) {  // strict Armijo test (:361)
         n_iter[l] += 1;
@@ -743,6 +872,7 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w,
     }
 }
 
+template <bool U0Z>
 __global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                      const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
@@ -755,13 +885,15 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
     const Dyn m(mm);
-    trial_solver(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
-                 retry_list + rg.lo, counter, hist_cost, l, Bp, N);
+    GYM_TRACE_WAVE(1);
+    trial_solver<U0Z>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+                      retry_list + rg.lo, counter, hist_cost, l, Bp, N);
 }
 
 // One pipeline phase: the first nb_b workgroups run the backward sweep of one half, the rest run the
 // Armijo trial of the other half.  The sweep is HBM-bound and the trial fp64-VALU-bound, so co-resident
 // waves of the two kinds overlap memory and arithmetic on every CU.  The two halves' lanes are disjoint.
+template <bool U0Z>
 __global__ __launch_bounds__(BLK, 4) void k_nt_phase(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                      const double2* __restrict__ xb_in,
                                                      const double* __restrict__ ub_in, int kb, int nb_b,
@@ -778,16 +910,17 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(gym_model mm, gym_weights w
     if ((int)blockIdx.x < nb_b) {
         const int64_t l = rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
         if (l >= rb.hi || status[l] != GYM_ACTIVE) return;
-        backward_solver(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len);
+        backward_solver<U0Z>(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len);
     } else {
         const int64_t l = rt.lo + (int64_t)(blockIdx.x - nb_b) * BLK + threadIdx.x;
         if (l >= rt.hi || status[l] != GYM_ACTIVE) return;
-        trial_solver(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
-                     retry_list + rt.lo, counter, hist_cost, l, Bp, N);
+        trial_solver<U0Z>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+                          retry_list + rt.lo, counter, hist_cost, l, Bp, N);
     }
 }
 
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
+template <bool U0Z>
 __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                        const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                        const double* __restrict__ xr, const double* __restrict__ ur,
@@ -805,13 +938,14 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
         const double2 xa = io.x[l], xb = io.x[Bp + l];
-        const double Jn = rollout_cform<false>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x, xa.y,
-                                               xb.x, xb.y);
+        const double Jn = rollout_cform<false, U0Z>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x,
+                                                    xa.y, xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
     }
 }
 
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
+template <bool U0Z>
 __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
                                                   const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
@@ -840,8 +974,8 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, S
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
         const double2 xa = io.x[l], xb = io.x[Bp + l];
-        const double Jn = rollout_cform<true>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y, xb.x,
-                                              xb.y);
+        const double Jn = rollout_cform<true, U0Z>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y,
+                                                   xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -891,19 +1025,23 @@ __global__ __launch_bounds__(STAT_THREADS) void k_stats_partial(const int32_t* _
 }
 
 // stats_out[0..7] = this range's statistics; if other != NULL, total[s] = other[s] + stats_out[s].
-__global__ void k_stats_final(const double* __restrict__ partials, int32_t* __restrict__ counter,
-                              double* __restrict__ stats_out, const double* __restrict__ other,
-                              double* __restrict__ total, int nblocks) {
-    const int s = threadIdx.x;
-    if (s < NSTAT) {
-        double v = 0.0;
-        for (int b = 0; b < nblocks; ++b) v += partials[(int64_t)b * NSTAT + s];
+// One wavefront per statistic: lane i adds partials i, i+64, ... in order, then a fixed shuffle tree.
+__global__ __launch_bounds__(64 * NSTAT) void k_stats_final(const double* __restrict__ partials,
+                                                            int32_t* __restrict__ counter,
+                                                            double* __restrict__ stats_out,
+                                                            const double* __restrict__ other,
+                                                            double* __restrict__ total, int nblocks) {
+    const int s = threadIdx.x / 64, ln = threadIdx.x % 64;
+    double v = 0.0;
+    for (int b = ln; b < nblocks; b += 64) v += partials[(int64_t)b * NSTAT + s];
+    v = wave_sum(v);
+    if (ln == 0) {
         if (s == 4) v = (double)(*counter);
         stats_out[s] = v;
         if (other) total[s] = other[s] + v;
     }
     __syncthreads();
-    if (s == 0) *counter = 0;  // the retry list is rebuilt every iteration
+    if (threadIdx.x == 0) *counter = 0;  // the retry list is rebuilt every iteration
 }
 
 __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restrict__ res_buf, int64_t B, int k_done) {
@@ -954,7 +1092,12 @@ struct TimedLaunch {  // records a start/stop event pair around one launch if th
     }
 };
 
-inline bool bad_dims(int64_t B, int64_t Bp, int N) { return B <= 0 || Bp < B || (Bp % 64) != 0 || N < 2; }
+// kernel instantiation for the batch's tau1 mode (GYM_FLAG_U0_ZERO)
+#define U0Z_SEL(b, kern) (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true> : kern<false>)
+
+inline bool bad_dims(int64_t B, int64_t Bp, int N) {
+    return B <= 0 || Bp < B || (Bp % 64) != 0 || Bp > GYM_MAX_BP || N < 2;
+}
 
 inline int launch_status() { return (int)hipGetLastError(); }
 
@@ -1106,6 +1249,10 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     const int T = b->N - 1;
     hipError_t e = hipMemsetAsync(b->u[0], 0, sizeof(double) * 2 * (size_t)T * b->Bp, st);
     if (e != hipSuccess) return (int)e;
+    if (b->flags & GYM_FLAG_U0_ZERO) {  // the trials never write the u0 planes: keep both buffers' zero
+        e = hipMemsetAsync(b->u[1], 0, sizeof(double) * 2 * (size_t)T * b->Bp, st);
+        if (e != hipSuccess) return (int)e;
+    }
     e = hipMemsetAsync(b->counters, 0, sizeof(int32_t) * 4, st);
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(b->stats, 0, sizeof(double) * 24, st);
@@ -1127,18 +1274,18 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
         {
             TimedLaunch tl(b->timing, 2, st);
             const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
-            hipLaunchKernelGGL(k_nt_candidates, dim3(gc), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref, b->u_ref,
+            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref, b->u_ref,
                                b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(k_nt_retry, dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref,
+        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref,
                            b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
                            b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
     }
     TimedLaunch tl(b->timing, 4, st);
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
                        b->n_iter, b->n_roll, b->partials, rg, c.k);
-    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64), 0, st, b->partials, counter, stats_out, other, total,
+    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64 * NSTAT), 0, st, b->partials, counter, stats_out, other, total,
                        STAT_BLOCKS);
 }
 
@@ -1160,14 +1307,14 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     const bool hist = a->record_history != 0;
     {
         TimedLaunch tl(b->timing, 0, st);
-        hipLaunchKernelGGL(k_nt_backward, dim3(grid), dim3(BLK), 0, st, *m, *w, io.x, io.u, b->x_ref, b->u_ref,
+        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, *m, *w, io.x, io.u, b->x_ref, b->u_ref,
                            (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
                            hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     {
         TimedLaunch tl(b->timing, 1, st);
-        hipLaunchKernelGGL(k_nt_trial, dim3(grid), dim3(BLK), 0, st, *m, *w, c, io, (const double2*)b->K1,
+        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, *m, *w, c, io, (const double2*)b->K1,
                            (const double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
                            all, b->Bp, b->N);
@@ -1203,7 +1350,7 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
     const TrialIO io = trial_io(b, kt < 0 ? 0 : kt);
     if (nb_b + nb_t > 0) {
         TimedLaunch tl(b->timing, (p & 1) ? 5 : 6, st);
-        hipLaunchKernelGGL(k_nt_phase, dim3(nb_b + nb_t), dim3(BLK), 0, st, *m, *w, c, io,
+        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, *m, *w, c, io,
                            (const double2*)b->x[kb & 1], b->u[kb & 1], kb, nb_b, rb, rt, (double2*)b->K1,
                            (double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters + ht,
@@ -1238,6 +1385,12 @@ int gym_newton_sigma(const gym_weights* w, const gym_batch* b, double* sig_out, 
                        (const double2*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
     return launch_status();
 }
+
+#ifdef GYM_WAVE_TRACE
+int gym_debug_wave_trace(void* host_out) {   // diagnostic build only: 2 x 8192 x 4 uint64
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wave_trace), sizeof(g_wave_trace));
+}
+#endif
 
 int gym_timing_create(gym_timing* t) {
     if (!t) return GYM_EINVAL;

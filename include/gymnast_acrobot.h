@@ -38,7 +38,14 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 1
+#define GYM_ABI_VERSION 2
+#define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
+
+/* gym_batch.flags */
+#define GYM_FLAG_U0_ZERO 1  /* u_ref[:,0] == 0: the unactuated tau1 channel stays exactly zero (u0 starts
+                             * at 0 and sigma0 = -(u0 - ur0) = -0, dynamics.py:205 ignores it), so the
+                             * solver neither reads nor writes its planes; both u buffers are zeroed by
+                             * gym_newton_init. Results are bit-identical to the general path.          */
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 
 /* Lane status codes (per-lane outcome of newton_Algorithm, trajectory_generation.py:329-396). */
@@ -87,6 +94,7 @@ typedef struct gym_timing {
 typedef struct gym_batch {
     int64_t B, Bp;      /* lanes, lane stride (multiple of 64)                     */
     int32_t N, hist_len;/* knots (T = N-1); rows of the optional history buffers   */
+    int32_t flags, pad; /* GYM_FLAG_*                                               */
     double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered   */
     double* u[2];       /* (T,2,Bp) control planes, double-buffered               */
     double* K1;         /* (T,2,Bp) double2 feedback gains, row 1                 */

@@ -25,7 +25,7 @@ def test_library_builds_and_exports_every_declared_symbol():
     assert declared and set(declared) == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.gym_abi_version() == 1
+    assert lib.gym_abi_version() == _lib.ABI_VERSION
     out = subprocess_nm(path)
     for name in declared:
         assert name in out, f"{name} not exported by {path}"

@@ -31,7 +31,7 @@ def test_native_library_is_loaded(eng):
     import ctypes
     from gymnast_optimalcontrol_amd import _lib
     assert eng.lib._name == _lib.LIB_PATH
-    assert ctypes.CDLL(_lib.LIB_PATH).gym_abi_version() == 1
+    assert ctypes.CDLL(_lib.LIB_PATH).gym_abi_version() == _lib.ABI_VERSION
 
 
 # ------------------------------------------------------------------------------ primitives
@@ -316,3 +316,30 @@ def test_pipelined_schedule_matches_serial(task2_refs, max_iters):
     if max_iters == 5000:
         assert (rs.status.cpu().numpy() == 2).sum() >= 2        # the batch exercises LS failures
         assert ls[:, 4].sum() > 0                               # ... and Armijo retries
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_u0_zero_stream_skipping_is_bitwise_identical(task2_refs, pipeline):
+    """GYM_FLAG_U0_ZERO (u_ref[:,0] == 0: tau1 planes neither read nor written) gives bitwise the general
+    path's results, incl. backtracking / LS-failure / NaN lanes; it is refused when u_ref[:,0] != 0."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    assert (ur[:, 0] == 0).all()
+    B = 700
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(33).uniform(-1.5, 1.5, (B, 2))
+    x0[3] = np.nan
+    eng = AcrobotEngine()
+    sz = BatchedNewtonSolver(eng, xr, ur, B, tol=1e-4, gamma_0=0.1, pipeline=pipeline)
+    sg = BatchedNewtonSolver(eng, xr, ur, B, tol=1e-4, gamma_0=0.1, pipeline=pipeline, u0_zero=False)
+    assert sz.u0_zero and not sg.u0_zero
+    rz, rg = sz.solve(x0, 5000, keep_stats=True), sg.solve(x0, 5000, keep_stats=True)
+    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma"):
+        a, b = getattr(rz, name).cpu().numpy(), getattr(rg, name).cpu().numpy()
+        assert np.array_equal(a, b, equal_nan=True), name
+    assert (rz.u.cpu().numpy()[:, :, 0] == 0).all()
+    assert np.array_equal(np.asarray(rz.stats_log), np.asarray(rg.stats_log), equal_nan=True)
+    ur1 = ur.copy(); ur1[5, 0] = 0.25
+    assert not BatchedNewtonSolver(eng, xr, ur1, 4).u0_zero
+    with pytest.raises(ValueError):
+        BatchedNewtonSolver(eng, xr, ur1, 4, u0_zero=True)

@@ -20,8 +20,9 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = name.replace("(anonymous namespace)::", "")
-    return n.split("(")[0].split("::")[-1].strip()
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    n = n.split("(")[0].split("::")[-1].strip()
+    return n.split("<")[0]          # k_nt_phase<true> -> k_nt_phase
 
 
 def load_pmc(path):
@@ -54,7 +55,7 @@ def main():
         for r in csv.DictReader(open(stats_csv)):
             kstats.append((short(r["Name"]), int(r["Calls"]), float(r["AverageNs"]), float(r["Percentage"])))
     pmc = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_valu"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_valu", "pmc_stall"):
         for (k, c), v in load_pmc(os.path.join(src, sub, "run_counter_collection.csv")).items():
             pmc.setdefault(k, {})[c] = {"mean": sum(v) / len(v), "n": len(v)}
     json.dump(pmc, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
