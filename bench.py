@@ -83,6 +83,70 @@ def cpu_baseline(x0, x_ref, u_ref, lanes: int, max_iters: int):
             "seconds": dt, "lane_iterations": its}
 
 
+def run_mpc(a):
+    """BASELINE cfg 5: batched receding-horizon MPC (trajectory_tracking.py:8-69 / main.py task_4).
+
+    One step = the whole tracking run of a.batch disturbed initial states: the exact per-control-step QP
+    solutions of all 500 windows (gym_tv_lqr_gains; horizon a.horizon) plus the batched closed-loop RK4
+    simulation under them (gym_track_rollout) and the lane-major results.  value = lanes x 500 control
+    steps / seconds per step."""
+    import torch
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine  # noqa: F401
+    g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))   # acrobot_optimal_trajectory
+    x_ref, u_ref = g["x"], g["u"]
+    N = x_ref.shape[0]
+    B = a.batch
+    x0 = x_ref[0] + np.random.default_rng(0).uniform(-0.1, 0.1, (B, 4))
+    x0[0] = x_ref[0] + 0.1                                      # main.task_4's disturbance
+    eng = tt._eng()
+    x0d, xrd, urd = eng.t(x0), eng.t(x_ref), eng.t(u_ref)
+    for _ in range(a.warmup):
+        tt.solve_mpc_tracking_batch(x0d, xrd, urd, a.horizon)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        x, u, K0 = tt.solve_mpc_tracking_batch(x0d, xrd, urd, a.horizon)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    steps = B * (N - 1)
+    # per-kernel times (HIP events on the engine's stream = torch's current stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    K0, QT = tt.mpc_gains(xrd, urd, a.horizon)
+    ev[1].record()
+    xs, us = eng.track_rollout(x0d, xrd, urd, K0)
+    ev[2].record()
+    torch.cuda.synchronize()
+    t_gain, t_roll = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    roll_bytes = B * (N * 32 + (N - 1) * 16 + 32)                 # x (pairs) + u (planes) written, x0 read
+    out = {"metric": "receding-horizon MPC control steps/s (BASELINE cfg 5)", "value": steps / dt,
+           "unit": "control steps/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * dt,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"cfg5: {B} disturbed initial states (x_ref[0] + U(-0.1,0.1)^4) x 500 control "
+                                  f"steps, horizon {a.horizon}, exact QP solution per step, RK4 plant",
+                      "lanes": B, "horizon": a.horizon, "control_steps": N - 1},
+           "kernels": {"mpc_gains_ms": t_gain, "track_rollout_ms": t_roll},
+           "roofline": {"bound": "hbm", "kernel": "track_rollout", "achieved": roll_bytes / (t_roll * 1e-3) / 1e9,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": roll_bytes / (t_roll * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "note": "latency-bound: B/64 wavefronts each run 500 dependent RK4 steps; the bytes are "
+                                "the trajectories written"}}
+    from oracle import tracking_np as tr
+    lanes = min(B, a.cpu_lanes)
+    t1 = time.perf_counter()
+    xo, uo, K0o = tr.solve_mpc_tracking(x0[:lanes], x_ref, u_ref, a.horizon)
+    tc = time.perf_counter() - t1
+    out["cpu_baseline"] = {"value": lanes * (N - 1) / tc, "unit": "control steps/s", "cores": 1, "kind": "port",
+                           "sample": f"first {lanes} lanes, numpy restatement (oracle/tracking_np.py) with the "
+                                     f"window QPs solved by the same Riccati recursion", "seconds": tc}
+    xg = x[:lanes].cpu().numpy()
+    out["parity"] = {"rel_l2_x_vs_oracle": float(np.linalg.norm(xg - xo) / np.linalg.norm(xo)),
+                     "rel_l2_K0_vs_oracle": float(np.linalg.norm(K0.cpu().numpy() - K0o) / np.linalg.norm(K0o)),
+                     "lane0_final_state": x[0, -1].cpu().numpy().tolist(), "tolerance": 1e-9}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,9 +160,14 @@ def main():
     ap.add_argument("--sync-every", type=int, default=4,
                     help="outer iterations between host reads of the (all-reduced) statistics; iterations "
                          "enqueued after every lane has finished are no-ops")
+    ap.add_argument("--workload", choices=("newton", "mpc"), default="newton",
+                    help="newton: the north-star metric (cfg 3); mpc: BASELINE cfg 5 (use --batch 8192)")
+    ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined"), default="auto",
                     help="solver schedule (auto: the solver's choice for the batch size)")
     a = ap.parse_args()
+    if a.workload == "mpc":
+        return run_mpc(a)
 
     import torch
     from gymnast_optimalcontrol_amd import distributed as gd

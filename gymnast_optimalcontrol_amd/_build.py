@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB_NAME = "libgymnast_acrobot.so"
 LIB_PATH = os.path.join(PKG, LIB_NAME)
-SOURCES = [os.path.join(CSRC, "acrobot_kernels.hip")]
+SOURCES = [os.path.join(CSRC, "acrobot_kernels.hip"), os.path.join(CSRC, "tracking_kernels.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "acrobot_device.hpp"), os.path.join(INCLUDE, "gymnast_acrobot.h")]
 ARCH = os.environ.get("GYM_OFFLOAD_ARCH", "gfx950")
 

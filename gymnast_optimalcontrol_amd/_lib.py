@@ -24,6 +24,7 @@ EXPORTS = (
     "gym_riccati_general",
     "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase",
     "gym_newton_finalize", "gym_newton_sigma",
+    "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_lq_forward", "gym_track_rollout",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even")
@@ -90,6 +91,10 @@ _SIGS = {
     "gym_newton_phase": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_finalize": [_WP, _BP, _I32, _P, _P, _P, _P, _P],
     "gym_newton_sigma": [_WP, _BP, _P, _P],
+    "gym_tv_lqr_gains": [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _D, _P, _P],
+    "gym_dare_fixed_point": [_P, _P, _P, _P, _I32, _D, _P, _P, _P],
+    "gym_lq_forward": [_P, _P, _I32, _P, _P, _I32, _D, _P, _P, _I32, _P, _P, _P],
+    "gym_track_rollout": [_MP, _P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _P],
     "gym_timing_create": [C.POINTER(GymTiming)],
     "gym_timing_destroy": [C.POINTER(GymTiming)],
     "gym_timing_collect": [C.POINTER(GymTiming)],

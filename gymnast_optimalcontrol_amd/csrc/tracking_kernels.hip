@@ -1,0 +1,233 @@
+// MI355X (gfx950) kernels of the LQR / receding-horizon MPC trackers (trajectory_tracking.py), C-ABI part 2.
+//
+// Both trackers follow ONE reference trajectory that every lane shares (main.py task_3 / task_4), so their
+// feedback gains are lane-independent:
+//   * LQR (solve_LQR_tracking :170-203): one backward recursion along the reference;
+//   * MPC (solve_mpc_tracking :8-69 with solver_mpc :73-140): at control step t the QP over the window
+//     [t, t + T_pred - 1] of the shifted reference (padded with (A_f, B_f)) has only equality constraints
+//     (test_constraints = False, :87), so its exact solution is u_0 = K_0(t) x_0 with K_0(t) the first gain of
+//     the window's finite-horizon LQ recursion.  All T windows are solved in parallel, one thread each.
+// The batched part is the closed-loop RK4 simulation of B perturbed initial states under the shared
+// feed-forward / feedback sequence (simulate_tracking :206-216 and the MPC loop :43-60), one lane per thread
+// with the gains, reference and feed-forward read through wave-uniform (scalar) loads.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "acrobot_device.hpp"
+#include "gymnast_acrobot.h"
+
+using gym::Dyn;
+
+namespace {
+
+struct M44 { double v[16]; };
+struct M22 { double v[4]; };
+
+// one step of the reference's recursion (trajectory_tracking.py:158-160 / :195-200):
+//   aux1 = R + B'PB, aux2 = B'PA, K = -inv(aux1) aux2, P <- Q + A'PA + (A'PB) K
+__device__ __forceinline__ void lqr_step(const double* A, const double* Bm, double* P, const M44& Q, const M22& R,
+                                         double* K) {
+    double PA[16], PB[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            PA[4 * i + j] = ((P[4 * i] * A[j] + P[4 * i + 1] * A[4 + j]) + P[4 * i + 2] * A[8 + j]) + P[4 * i + 3] * A[12 + j];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            PB[2 * i + j] = ((P[4 * i] * Bm[j] + P[4 * i + 1] * Bm[2 + j]) + P[4 * i + 2] * Bm[4 + j]) + P[4 * i + 3] * Bm[6 + j];
+    }
+    double a1[4], a2[8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            a1[2 * i + j] = R.v[2 * i + j] + (((Bm[i] * PB[j] + Bm[2 + i] * PB[2 + j]) + Bm[4 + i] * PB[4 + j]) + Bm[6 + i] * PB[6 + j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            a2[4 * i + j] = ((Bm[i] * PA[j] + Bm[2 + i] * PA[4 + j]) + Bm[4 + i] * PA[8 + j]) + Bm[6 + i] * PA[12 + j];
+    }
+    const double idet = 1.0 / (a1[0] * a1[3] - a1[1] * a1[2]);
+    const double i00 = a1[3] * idet, i01 = -a1[1] * idet, i10 = -a1[2] * idet, i11 = a1[0] * idet;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        K[j] = -(i00 * a2[j] + i01 * a2[4 + j]);
+        K[4 + j] = -(i10 * a2[j] + i11 * a2[4 + j]);
+    }
+    double nP[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double apa = ((A[i] * PA[j] + A[4 + i] * PA[4 + j]) + A[8 + i] * PA[8 + j]) + A[12 + i] * PA[12 + j];
+            const double apb0 = ((A[i] * PB[0] + A[4 + i] * PB[2]) + A[8 + i] * PB[4]) + A[12 + i] * PB[6];
+            const double apb1 = ((A[i] * PB[1] + A[4 + i] * PB[3]) + A[8 + i] * PB[5]) + A[12 + i] * PB[7];
+            nP[4 * i + j] = (Q.v[4 * i + j] + apa) + (apb0 * K[j] + apb1 * K[4 + j]);
+        }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) P[k] = nP[k];
+}
+
+// stage s of a stage array (continuous Jacobians if disc: A_d = I + dt A_c, B_d = dt B_c, :161-164)
+__device__ __forceinline__ void load_stage(const double* A, const double* Bm, int s, int S, const double* Ap,
+                                           const double* Bp, int disc, double dt, double* Ad, double* Bd) {
+    const double* a = s < S ? A + 16 * (int64_t)s : Ap;
+    const double* b = s < S ? Bm + 8 * (int64_t)s : Bp;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) Ad[k] = disc ? ((k % 5 == 0 ? 1.0 : 0.0) + dt * a[k]) : a[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) Bd[k] = disc ? dt * b[k] : b[k];
+}
+
+// window w: recursion over stages w + L-2 .. w (stage index >= S -> pad), terminal P = QT.
+// all_gains: K_out (L-1, 2, 4) of window 0;  else K_out (nwin, 2, 4) = the first gain of every window.
+__global__ __launch_bounds__(64) void k_tv_lqr_gains(const double* __restrict__ A, const double* __restrict__ Bm,
+                                                     int S, const double* __restrict__ Ap,
+                                                     const double* __restrict__ Bp, M44 Q, M22 R, M44 QT, int L,
+                                                     int nwin, int all_gains, int disc, double dt,
+                                                     double* __restrict__ K_out) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwin) return;
+    double P[16], K[8], Ad[16], Bd[8];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) P[k] = QT.v[k];
+    for (int s = L - 2; s >= 0; --s) {
+        load_stage(A, Bm, w + s, S, Ap, Bp, disc, dt, Ad, Bd);
+        lqr_step(Ad, Bd, P, Q, R, K);
+        if (all_gains) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) K_out[8 * (int64_t)s + k] = K[k];
+        }
+    }
+    if (!all_gains) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) K_out[8 * (int64_t)w + k] = K[k];
+    }
+}
+
+// compute_P_inf (:144-165): P <- Riccati map of (A, B, Q, R) from P = Q until max|dP| < tol (single thread)
+__global__ void k_dare_fixed_point(const double* __restrict__ A, const double* __restrict__ Bm, M44 Q, M22 R,
+                                   int max_iter, double tol, double* __restrict__ P_out, int32_t* __restrict__ iters) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double a[16], b[8], P[16], K[8];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { a[k] = A[k]; P[k] = Q.v[k]; }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = Bm[k];
+    int it = max_iter;
+    for (int i = 0; i < max_iter; ++i) {
+        double prev[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) prev[k] = P[k];
+        lqr_step(a, b, P, Q, R, K);
+        double d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d = fmax(d, fabs(P[k] - prev[k]));
+        if (d < tol) { it = i + 1; break; }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) P_out[k] = P[k];
+    *iters = it;
+}
+
+// LQ forward pass of one window (solver_mpc's X_opt, U_opt): x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s
+__global__ void k_lq_forward(const double* __restrict__ A, const double* __restrict__ Bm, int S,
+                             const double* __restrict__ Ap, const double* __restrict__ Bp, int disc, double dt,
+                             const double* __restrict__ K, const double* __restrict__ x0, int L,
+                             double* __restrict__ X, double* __restrict__ U) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double x[4] = {x0[0], x0[1], x0[2], x0[3]}, Ad[16], Bd[8];
+    for (int s = 0; s < L - 1; ++s) {
+        const double* k = K + 8 * s;
+        const double u0 = ((k[0] * x[0] + k[1] * x[1]) + k[2] * x[2]) + k[3] * x[3];
+        const double u1 = ((k[4] * x[0] + k[5] * x[1]) + k[6] * x[2]) + k[7] * x[3];
+        X[4 * s] = x[0]; X[4 * s + 1] = x[1]; X[4 * s + 2] = x[2]; X[4 * s + 3] = x[3];
+        U[2 * s] = u0; U[2 * s + 1] = u1;
+        load_stage(A, Bm, s, S, Ap, Bp, disc, dt, Ad, Bd);
+        double n[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            n[i] = (((Ad[4 * i] * x[0] + Ad[4 * i + 1] * x[1]) + Ad[4 * i + 2] * x[2]) + Ad[4 * i + 3] * x[3]) +
+                   (Bd[2 * i] * u0 + Bd[2 * i + 1] * u1);
+        x[0] = n[0]; x[1] = n[1]; x[2] = n[2]; x[3] = n[3];
+    }
+    X[4 * (L - 1)] = x[0]; X[4 * (L - 1) + 1] = x[1]; X[4 * (L - 1) + 2] = x[2]; X[4 * (L - 1) + 3] = x[3];
+}
+
+// Batched closed-loop tracking simulation (simulate_tracking :206-216; MPC loop :43-60):
+//   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
+// x0 (B,4) lane-major; shared x_ff (N,4), u_ff (T,2), K (T,2,4); out x (N,2,Bp) pairs, u (T,2,Bp) planes.
+__global__ __launch_bounds__(64) void k_track_rollout(gym_model mm, const double* __restrict__ x0,
+                                                      const double* __restrict__ x_ff, const double* __restrict__ u_ff,
+                                                      const double* __restrict__ K, int64_t B, int64_t Bp, int N,
+                                                      double2* __restrict__ xo, double* __restrict__ uo) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= B) return;
+    const Dyn m(mm);
+    const int T = N - 1;
+    double n0 = x0[4 * l], n1 = x0[4 * l + 1], n2 = x0[4 * l + 2], n3 = x0[4 * l + 3];
+    xo[l] = make_double2(n0, n1);
+    xo[Bp + l] = make_double2(n2, n3);
+    for (int t = 0; t < T; ++t) {
+        const double* k = K + 8 * t;
+        const double* xr = x_ff + 4 * t;
+        const double d0 = n0 - xr[0], d1 = n1 - xr[1], d2 = n2 - xr[2], d3 = n3 - xr[3];
+        const double v0 = u_ff[2 * t] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
+        const double v1 = u_ff[2 * t + 1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+        uo[(2 * (int64_t)t) * Bp + l] = v0;
+        uo[(2 * (int64_t)t + 1) * Bp + l] = v1;
+        gym::rk4(m, n0, n1, n2, n3, v1);
+        xo[(2 * (int64_t)(t + 1)) * Bp + l] = make_double2(n0, n1);
+        xo[(2 * (int64_t)(t + 1) + 1) * Bp + l] = make_double2(n2, n3);
+    }
+}
+
+inline M44 m44(const double* p) { M44 m; for (int i = 0; i < 16; ++i) m.v[i] = p[i]; return m; }
+inline M22 m22(const double* p) { M22 m; for (int i = 0; i < 4; ++i) m.v[i] = p[i]; return m; }
+inline int launch_status() { return (int)hipGetLastError(); }
+
+}  // namespace
+
+extern "C" {
+
+int gym_tv_lqr_gains(const double* A, const double* Bm, int32_t S, const double* A_pad, const double* B_pad,
+                     const double Q[16], const double R[4], const double QT[16], int32_t L, int32_t nwin,
+                     int32_t all_gains, int32_t discretize, double dt, double* K_out, void* s) {
+    if (!A || !Bm || !Q || !R || !QT || !K_out || S <= 0 || L < 2 || nwin <= 0 || (all_gains && nwin != 1))
+        return GYM_EINVAL;
+    if ((nwin - 1) + (L - 2) >= S && (!A_pad || !B_pad)) return GYM_EINVAL;   // a window runs past the stages
+    hipLaunchKernelGGL(k_tv_lqr_gains, dim3((nwin + 63) / 64), dim3(64), 0, (hipStream_t)s, A, Bm, S, A_pad, B_pad,
+                       m44(Q), m22(R), m44(QT), L, nwin, all_gains, discretize, dt, K_out);
+    return launch_status();
+}
+
+int gym_dare_fixed_point(const double* A, const double* Bm, const double Q[16], const double R[4], int32_t max_iter,
+                         double tol, double* P_out, int32_t* iters_out, void* s) {
+    if (!A || !Bm || !Q || !R || !P_out || !iters_out || max_iter <= 0) return GYM_EINVAL;
+    hipLaunchKernelGGL(k_dare_fixed_point, dim3(1), dim3(64), 0, (hipStream_t)s, A, Bm, m44(Q), m22(R), max_iter, tol,
+                       P_out, iters_out);
+    return launch_status();
+}
+
+int gym_lq_forward(const double* A, const double* Bm, int32_t S, const double* A_pad, const double* B_pad,
+                   int32_t discretize, double dt, const double* K, const double* x0, int32_t L, double* X, double* U,
+                   void* s) {
+    if (!A || !Bm || !K || !x0 || !X || !U || S <= 0 || L < 2) return GYM_EINVAL;
+    if (L - 2 >= S && (!A_pad || !B_pad)) return GYM_EINVAL;
+    hipLaunchKernelGGL(k_lq_forward, dim3(1), dim3(64), 0, (hipStream_t)s, A, Bm, S, A_pad, B_pad, discretize, dt, K,
+                       x0, L, X, U);
+    return launch_status();
+}
+
+int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
+                      int64_t B, int64_t Bp, int32_t N, double* x_out, double* u_out, void* s) {
+    if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || Bp < B || (Bp % 64) != 0 ||
+        Bp > GYM_MAX_BP || N < 2)
+        return GYM_EINVAL;
+    hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, *m, x0, x_ff,
+                       u_ff, K, B, Bp, N, (double2*)x_out, u_out);
+    return launch_status();
+}
+
+}  // extern "C"

@@ -287,3 +287,67 @@ class AcrobotEngine:
                                                 self.stream), "gym_riccati_general")
         return (K[..., :B].permute(2, 0, 1).reshape(B, T, 2, 4), sg[..., :B].permute(2, 0, 1).contiguous(),
                 dJ[:B])
+
+    # ------------------------------------------------------------------ LQR / MPC trackers
+    @staticmethod
+    def _host_mat(M, n, name):
+        M = np.ascontiguousarray(np.asarray(M, dtype=np.float64))
+        if M.shape != (n, n):
+            raise ValueError(f"{name} must be {n}x{n}, got {M.shape}")
+        return M
+
+    def tv_lqr_gains(self, A, Bm, Q, R, QT, L: int, nwin: int = 1, all_gains: bool = True, A_pad=None,
+                     B_pad=None, discretize: bool = False) -> torch.Tensor:
+        """Windowed time-varying LQR gains (gym_tv_lqr_gains): stages A (S,4,4), B (S,4,2) on the device.
+        all_gains: (L-1,2,4) gains of window 0; else (nwin,2,4) first gains of windows 0..nwin-1."""
+        A = self.t(A).reshape(-1, 4, 4); Bm = self.t(Bm).reshape(-1, 4, 2)
+        S = A.shape[0]
+        Ap = None if A_pad is None else self.t(A_pad).reshape(4, 4)
+        Bp_ = None if B_pad is None else self.t(B_pad).reshape(4, 2)
+        Qh, Rh, QTh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R"), self._host_mat(QT, 4, "Q_T")
+        out = torch.empty(((L - 1) if all_gains else nwin, 2, 4), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_tv_lqr_gains(A.data_ptr(), Bm.data_ptr(), S, _lib.ptr(Ap), _lib.ptr(Bp_),
+                                             Qh.ctypes.data, Rh.ctypes.data, QTh.ctypes.data, int(L), int(nwin),
+                                             int(bool(all_gains)), int(bool(discretize)), self.dt, out.data_ptr(),
+                                             self.stream), "gym_tv_lqr_gains")
+        return out
+
+    def dare_fixed_point(self, A, Bm, Q, R, max_iter: int = 1000, tol: float = 1e-6):
+        """compute_P_inf on the device: returns (P (4,4) tensor, iterations)."""
+        A = self.t(A).reshape(4, 4); Bm = self.t(Bm).reshape(4, 2)
+        Qh, Rh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R")
+        P = torch.empty((4, 4), dtype=F64, device=self.device)
+        it = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.gym_dare_fixed_point(A.data_ptr(), Bm.data_ptr(), Qh.ctypes.data, Rh.ctypes.data,
+                                                 int(max_iter), float(tol), P.data_ptr(), it.data_ptr(), self.stream),
+                   "gym_dare_fixed_point")
+        return P, int(it.item())
+
+    def lq_forward(self, A, Bm, K, x0, L: int, A_pad=None, B_pad=None, discretize: bool = False):
+        """One window's LQ forward pass: X (L,4), U (L-1,2)."""
+        A = self.t(A).reshape(-1, 4, 4); Bm = self.t(Bm).reshape(-1, 4, 2)
+        Ap = None if A_pad is None else self.t(A_pad).reshape(4, 4)
+        Bp_ = None if B_pad is None else self.t(B_pad).reshape(4, 2)
+        K = self.t(K).reshape(-1, 2, 4); x0 = self.t(x0).reshape(4)
+        X = torch.empty((L, 4), dtype=F64, device=self.device)
+        U = torch.empty((L - 1, 2), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_lq_forward(A.data_ptr(), Bm.data_ptr(), A.shape[0], _lib.ptr(Ap), _lib.ptr(Bp_),
+                                           int(bool(discretize)), self.dt, K.data_ptr(), x0.data_ptr(), int(L),
+                                           X.data_ptr(), U.data_ptr(), self.stream), "gym_lq_forward")
+        return X, U
+
+    def track_rollout(self, x0, x_ff, u_ff, K):
+        """Batched closed-loop tracking: x0 (B,4) -> x (B,N,4), u (B,T,2) under the shared (x_ff, u_ff, K)."""
+        x0 = self.t(x0).reshape(-1, 4)
+        x_ff = self.t(x_ff).reshape(-1, 4); u_ff = self.t(u_ff).reshape(-1, 2); K = self.t(K).reshape(-1, 2, 4)
+        N = x_ff.shape[0]
+        if u_ff.shape[0] != N - 1 or K.shape[0] != N - 1:
+            raise ValueError(f"feed-forward / gains must hold {N - 1} stages, got {u_ff.shape[0]} / {K.shape[0]}")
+        B = x0.shape[0]
+        Bp = padded(B)
+        xs = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device)
+        us = torch.empty((N - 1, 2, Bp, 1), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_track_rollout(C.byref(self.model), x0.data_ptr(), x_ff.data_ptr(), u_ff.data_ptr(),
+                                              K.data_ptr(), B, Bp, N, xs.data_ptr(), us.data_ptr(), self.stream),
+                   "gym_track_rollout")
+        return self.unpack(xs, B), self.unpack(us, B)

@@ -207,6 +207,33 @@ int gym_newton_finalize(const gym_weights* w, const gym_batch* bt, int32_t k_don
 /* sigma (B,T,2) of each lane's most recent backward sweep (sigma1 from cs, sigma0 recomputed). */
 int gym_newton_sigma(const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);
 
+/* ---------------- LQR / receding-horizon MPC trackers (trajectory_tracking.py) ---------------- */
+/* Time-varying LQR gains over windows of a stage array.  Stages: A (S,4,4), B (S,4,2) [device], continuous
+ * Jacobians if discretize != 0 (A_d = I + dt A, B_d = dt B, trajectory_generation.py:161-164), stage index >= S
+ * reads the pad stage A_pad (4,4), B_pad (4,2) [device].  Window w runs the reference's recursion
+ * (trajectory_tracking.py:195-200)  aux1 = R + B'PB, aux2 = B'PA, K = -inv(aux1) aux2, P <- Q + A'PA + (A'PB) K
+ * over stages w+L-2 .. w from P = QT.  all_gains != 0 (nwin == 1): K_out (L-1,2,4) = every gain
+ * (solve_LQR_tracking :170-203 with L = S+1);  else K_out (nwin,2,4) = each window's first gain, the exact
+ * solution u0 = K x0 of solver_mpc's equality-constrained QP (:73-140, T_pred = L) at control step w
+ * (solve_mpc_tracking :8-69).  Q, R, QT [host].                                                                  */
+int gym_tv_lqr_gains(const double* A, const double* B, int32_t S, const double* A_pad, const double* B_pad,
+                     const double Q[16], const double R[4], const double QT[16], int32_t L, int32_t nwin,
+                     int32_t all_gains, int32_t discretize, double dt, double* K_out, void* stream);
+/* compute_P_inf (trajectory_tracking.py:144-165): P (4,4) and the iteration count [device outputs]; A, B discrete
+ * [device], Q, R [host]. */
+int gym_dare_fixed_point(const double* A, const double* B, const double Q[16], const double R[4], int32_t max_iter,
+                         double tol, double* P_out, int32_t* iters_out, void* stream);
+/* solver_mpc's X_opt (L,4), U_opt (L-1,2): forward pass x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s of one window
+ * (gains from gym_tv_lqr_gains with all_gains), x0 (4) [device]. */
+int gym_lq_forward(const double* A, const double* B, int32_t S, const double* A_pad, const double* B_pad,
+                   int32_t discretize, double dt, const double* K, const double* x0, int32_t L, double* X, double* U,
+                   void* stream);
+/* Batched closed-loop tracking (simulate_tracking :206-216; the MPC loop :43-60):
+ *   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
+ * x0 (B,4) lane-major; shared x_ff (N,4), u_ff (T,2), K (T,2,4); x_out (N,2,Bp) pairs, u_out (T,2,Bp) planes. */
+int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
+                      int64_t B, int64_t Bp, int32_t N, double* x_out, double* u_out, void* stream);
+
 /* [host] create / destroy the events of a gym_timing; collect = add the elapsed time of every pending
  * pair (call only after the stream that recorded them has been synchronised). */
 int gym_timing_create(gym_timing* t);

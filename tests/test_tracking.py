@@ -1,0 +1,136 @@
+"""LQR / receding-horizon MPC trackers (trajectory_tracking.py).
+
+Golden data: tests/golden/tracking.npz, produced by running the reference's own compute_P_inf,
+solve_LQR_tracking and simulate_tracking (tests/golden/make_golden_tracking.py).  The MPC's IPOPT QP
+(solver_mpc) cannot run here (casadi is absent): MPC parity is pinned to the exact solution of that
+equality-constrained QP (dense KKT solve in oracle/tracking_np.py), not to IPOPT's iterates.
+Tolerances: gains 1e-9 relative (same recursion, reordered 4x4 products), closed-loop trajectories 1e-9
+rel-L2.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, rel_l2
+
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def trk():
+    return load_golden("tracking")
+
+
+# ------------------------------------------------------------------------------ oracle (CPU)
+def test_oracle_lqr_matches_reference_golden(trk):
+    from oracle import tracking_np as tr
+    K = tr.solve_LQR_tracking(trk["x_opt"], trk["u_opt"])
+    assert np.abs(K - trk["K_reg"]).max() <= 1e-10 * np.abs(trk["K_reg"]).max()
+    x, u = tr.simulate_tracking(trk["x_opt"], trk["u_opt"], trk["K_reg"], trk["x_opt"][0][None] + trk["dx"][:, None])
+    assert rel_l2(x, trk["x_track"]) < 1e-12 and rel_l2(u, trk["u_track"]) < 1e-12
+
+
+def test_oracle_p_inf_matches_reference_golden(trk):
+    from oracle import tracking_np as tr
+    P, it = tr.compute_P_inf(trk["A_f"], trk["B_f"], trk["Q_mpc"], trk["R_mpc"])
+    np.testing.assert_array_equal(P, trk["P_inf"])
+    # SURVEY.md 8(c) KAT: diag(P_inf) ~ [2.257e7, 1.674e6, 3.202e6, 3.610e5]
+    np.testing.assert_allclose(np.diag(P), [2.257e7, 1.674e6, 3.202e6, 3.610e5], rtol=2e-3)
+
+
+@pytest.mark.parametrize("t", [0, 137, 430, 499])
+def test_oracle_mpc_gain_is_the_exact_qp_solution(trk, t):
+    """u0 = K_0(t) x0 equals the dense KKT solution of solver_mpc's QP for the window of control step t."""
+    from oracle import tracking_np as tr
+    A, B = tr.linearize_along(trk["x_opt"], trk["u_opt"])
+    QT, _ = tr.compute_P_inf(trk["A_f"], trk["B_f"], tr.Q_MPC, tr.R_MPC)
+    for Tp in (50, 75):
+        Aw, Bw = list(tr.mpc_windows(A, B, trk["A_f"], trk["B_f"], Tp, t + 1))[t]
+        K0 = tr.mpc_first_gain(Aw, Bw, tr.Q_MPC, tr.R_MPC, QT)
+        x0 = np.random.default_rng(t).uniform(-0.2, 0.2, 4)
+        U0, X, U = tr.mpc_qp_kkt(x0, Aw, Bw, tr.Q_MPC, tr.R_MPC, QT)
+        np.testing.assert_allclose(K0 @ x0, U0, rtol=1e-8, atol=1e-10 * max(1.0, np.abs(U0).max()))
+
+
+# ------------------------------------------------------------------------------ HIP path
+@pytest.mark.gpu
+def test_lqr_gains_and_tracking_match_reference(trk):
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    K = np.asarray(tt.solve_LQR_tracking(trk["x_opt"], trk["u_opt"]))
+    assert K.shape == (500, 2, 4)
+    assert np.abs(K - trk["K_reg"]).max() <= TOL * np.abs(trk["K_reg"]).max()
+    for i, dx in enumerate(trk["dx"]):
+        x, u = tt.LQR_tracking(trk["x_opt"], trk["u_opt"], trk["t_ref"], x0_perturbed=trk["x_opt"][0] + dx)
+        assert rel_l2(x, trk["x_track"][i]) < TOL and rel_l2(u, trk["u_track"][i]) < TOL
+
+
+@pytest.mark.gpu
+def test_lqr_batch_equals_single_lane(trk):
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    from oracle import tracking_np as tr
+    B = 200
+    x0 = trk["x_opt"][0] + np.random.default_rng(3).uniform(-0.3, 0.3, (B, 4))
+    x, u, K = tt.LQR_tracking_batch(trk["x_opt"], trk["u_opt"], x0)
+    xo, uo = tr.simulate_tracking(trk["x_opt"], trk["u_opt"], trk["K_reg"], x0)
+    assert rel_l2(x.cpu().numpy(), xo) < TOL and rel_l2(u.cpu().numpy(), uo) < TOL
+    xs, us = tt.simulate_tracking(trk["x_opt"], trk["u_opt"], list(K.cpu().numpy()), x0[7])   # same gains
+    np.testing.assert_array_equal(xs, x[7].cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_p_inf_on_device(trk):
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    P = tt.compute_P_inf(trk["A_f"], trk["B_f"], trk["Q_mpc"], trk["R_mpc"])
+    np.testing.assert_allclose(P, trk["P_inf"], rtol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T_pred", [50, 75])
+def test_mpc_gains_and_closed_loop_match_oracle(trk, T_pred):
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    from oracle import tracking_np as tr
+    K0, QT = tt.mpc_gains(trk["x_opt"], trk["u_opt"], T_pred)
+    K0o, QTo = tr.mpc_gains(trk["x_opt"], trk["u_opt"], T_pred)
+    np.testing.assert_allclose(QT.cpu().numpy(), QTo, rtol=1e-9)
+    assert np.abs(K0.cpu().numpy() - K0o).max() <= TOL * np.abs(K0o).max()
+    B = 65
+    x0 = trk["x_opt"][0] + np.random.default_rng(T_pred).uniform(-0.1, 0.1, (B, 4))
+    x0[0] = trk["x_opt"][0] + 0.1                       # main.task_4's disturbance
+    x, u, _ = tt.solve_mpc_tracking_batch(x0, trk["x_opt"], trk["u_opt"], T_pred)
+    xo, uo = tr.simulate_tracking(trk["x_opt"], trk["u_opt"], K0o, x0)
+    assert rel_l2(x.cpu().numpy(), xo) < TOL and rel_l2(u.cpu().numpy(), uo) < TOL
+    # reference-shaped entry point (task_4: T = len(t_ref))
+    xr, ur = tt.solve_mpc_tracking(x0[0], trk["x_opt"], trk["u_opt"], len(trk["t_ref"]), T_pred=T_pred)
+    assert xr.shape == trk["x_opt"].shape and ur.shape == trk["u_opt"].shape
+    np.testing.assert_array_equal(xr, x[0].cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_solver_mpc_window_matches_kkt(trk):
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    from oracle import tracking_np as tr
+    A, B = tr.linearize_along(trk["x_opt"], trk["u_opt"])
+    QT, _ = tr.compute_P_inf(trk["A_f"], trk["B_f"], tr.Q_MPC, tr.R_MPC)
+    Tp = 75
+    Aw, Bw = A[100:100 + Tp], B[100:100 + Tp]
+    x0 = np.array([0.05, -0.02, 0.1, 0.0])
+    U0, X, U = tt.solver_mpc(x0, list(Aw), list(Bw), tr.Q_MPC, tr.R_MPC, QT, Tp)
+    U0o, Xo, Uo = tr.mpc_qp_kkt(x0, Aw, Bw, tr.Q_MPC, tr.R_MPC, QT)
+    np.testing.assert_allclose(U0, U0o, rtol=1e-8, atol=1e-12)
+    assert X.shape == (Tp, 4) and U.shape == (Tp, 2)
+    assert rel_l2(X, Xo) < 1e-8 and rel_l2(U[:-1], Uo) < 1e-8
+
+
+@pytest.mark.gpu
+def test_tracking_abi_rejects_bad_arguments():
+    import ctypes as C
+    from gymnast_optimalcontrol_amd import _lib
+    lib = _lib.load()
+    Q = np.eye(4); R = np.eye(2)
+    # window past the end of the stages without a pad stage
+    assert lib.gym_tv_lqr_gains(1, 1, 10, None, None, Q.ctypes.data, R.ctypes.data, Q.ctypes.data, 20, 1, 1, 0,
+                                0.02, 1, None) == 1
+    # all_gains needs a single window
+    assert lib.gym_tv_lqr_gains(1, 1, 100, None, None, Q.ctypes.data, R.ctypes.data, Q.ctypes.data, 20, 2, 1, 0,
+                                0.02, 1, None) == 1
+    m = _lib.GymModel()
+    assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 100, 100, 501, 1, 1, None) == 1   # Bp not a multiple of 64
