@@ -23,15 +23,18 @@ EXPORTS = (
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
     "gym_riccati_general",
     "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase",
-    "gym_newton_finalize", "gym_newton_sigma",
+    "gym_newton_finalize", "gym_newton_fill_states", "gym_newton_sigma",
+    "gym_gamma_sweep", "gym_newton_gamma_sweep",
     "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_lq_forward", "gym_track_rollout",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even")
 
-ABI_VERSION = 2          # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 3          # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
+FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
+CKPT_INTERVAL = 4        # GYM_CKPT_INTERVAL
 
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4
 STATUS_NAMES = {ACTIVE: "active", CONVERGED: "converged", LS_FAILED: "ls_failed", MAX_ITERS: "max_iters", PAD: "pad"}
@@ -89,8 +92,11 @@ _SIGS = {
     "gym_newton_iteration": [_MP, _WP, _AP, _BP, _I32, _P],
     "gym_newton_pipeline_split": [_BP, C.POINTER(C.c_int64)],
     "gym_newton_phase": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
-    "gym_newton_finalize": [_WP, _BP, _I32, _P, _P, _P, _P, _P],
+    "gym_newton_finalize": [_MP, _WP, _BP, _I32, _P, _P, _P, _P, _P],
+    "gym_newton_fill_states": [_MP, _BP, _I32, _P],
     "gym_newton_sigma": [_WP, _BP, _P, _P],
+    "gym_gamma_sweep": [_MP, _WP, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I32, _P],
+    "gym_newton_gamma_sweep": [_MP, _WP, _BP, _I32, _P, _I32, _P, _P],
     "gym_tv_lqr_gains": [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _D, _P, _P],
     "gym_dare_fixed_point": [_P, _P, _P, _P, _I32, _D, _P, _P, _P],
     "gym_lq_forward": [_P, _P, _I32, _P, _P, _I32, _D, _P, _P, _I32, _P, _P, _P],

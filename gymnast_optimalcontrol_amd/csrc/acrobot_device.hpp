@@ -12,10 +12,13 @@ namespace gym {
 
 constexpr int kWave = 64;
 
-// Coefficients hoisted out of the time loop (uniform per launch).
+// Coefficients hoisted out of the time loop (uniform per launch).  Built on the host and passed to the
+// kernels by value, so they sit in SGPRs (kernel arguments) instead of occupying per-lane VGPRs; the
+// derived products are IEEE-rounded identically on host and device.
 struct Dyn {
     double b, d, a2b, bb, dad, g1, g2, f1, f2, h, h2, h6;
-    __device__ __forceinline__ explicit Dyn(const gym_model& m)
+    Dyn() = default;
+    __host__ __device__ __forceinline__ explicit Dyn(const gym_model& m)
         : b(m.b), d(m.d), a2b(m.a), bb(m.b * m.b), dad(m.d * (m.a - m.d)), g1(m.g1), g2(m.g2), f1(m.f1),
           f2(m.f2), h(m.dt), h2(m.dt * 0.5), h6(1.0 / 6.0) {}
 };

@@ -31,6 +31,47 @@ constexpr int BLK = 64;           // one wavefront per workgroup for the per-lan
 constexpr int STAT_BLOCKS = 256;  // first stage of the deterministic statistics reduction
 constexpr int STAT_THREADS = 256;
 constexpr int NSTAT = 8;
+constexpr int CKI = GYM_CKPT_INTERVAL;   // state checkpoint interval (GYM_FLAG_X_CKPT)
+
+// Cost weights as the kernels take them: the reference's diagonal Q, R, Q_T plus the Gauss-Newton
+// blocks' constants (Q_t = 2Q, R_t = 2R, G00 = 2 R0 and its inverse), formed once on the host so that
+// they are kernel arguments (SGPRs) rather than per-lane VGPRs.  2x is exact and 1/G00 correctly rounded
+// on both sides, so the values are those the device would compute.
+struct KW {
+    double Q[4], R[2], QT[4];
+    double twoQ[4], G00, twoR1, iG00;
+};
+static_assert(sizeof(Dyn) == 12 * sizeof(double) && sizeof(KW) == 17 * sizeof(double), "kernarg layout");
+
+// The solver kernels take (Dyn m, KW w, ...) as their FIRST two parameters, i.e. at byte offsets 0 and 96 of
+// the kernel argument segment.  Inside the stage loops the sweep re-reads them from there every stage with
+// scalar loads (the pointer is made opaque per call so the loads are not hoisted): they are then short-
+// lived SGPRs instead of 36 loop-invariant dwords that overflow the SGPR file, whose spills to VGPR lanes
+// cost one v_readlane (a VALU slot) per dword per stage.
+typedef const __attribute__((address_space(4))) double* kptr_t;
+struct KArgs {
+    Dyn m;
+    KW w;
+};
+__device__ __forceinline__ KArgs kernarg_consts() {
+    kptr_t p = (kptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    KArgs a;
+    a.m.b = p[0]; a.m.d = p[1]; a.m.a2b = p[2]; a.m.bb = p[3]; a.m.dad = p[4]; a.m.g1 = p[5]; a.m.g2 = p[6];
+    a.m.f1 = p[7]; a.m.f2 = p[8]; a.m.h = p[9]; a.m.h2 = p[10]; a.m.h6 = p[11];
+    for (int i = 0; i < 4; ++i) { a.w.Q[i] = p[12 + i]; a.w.QT[i] = p[18 + i]; a.w.twoQ[i] = p[22 + i]; }
+    a.w.R[0] = p[16]; a.w.R[1] = p[17];
+    a.w.G00 = p[26]; a.w.twoR1 = p[27]; a.w.iG00 = p[28];
+    return a;
+}
+
+inline KW kw(const gym_weights& w) {
+    KW k;
+    for (int i = 0; i < 4; ++i) { k.Q[i] = w.Q[i]; k.QT[i] = w.QT[i]; k.twoQ[i] = 2.0 * w.Q[i]; }
+    k.R[0] = w.R[0]; k.R[1] = w.R[1];
+    k.G00 = 2.0 * w.R[0]; k.twoR1 = 2.0 * w.R[1]; k.iG00 = 1.0 / k.G00;
+    return k;
+}
 
 typedef double d2v __attribute__((ext_vector_type(2)));
 
@@ -68,11 +109,13 @@ constexpr int kNT = 2;  // gfx950 cache-policy bits: nt (streamed once)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
+template <int CP = kNT>   // CP: cache policy (kNT for the read-once solver streams, 0 for re-read ones)
 __device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
-    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, kNT));
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, CP));
 }
+template <int CP = kNT>
 __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, kNT));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, CP));
 }
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a, double b) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, kNT);
@@ -82,6 +125,19 @@ __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint
 }
 
 __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
+
+// Progress-banded wave priority: every solver stream loop starts at priority 3 and steps down one level
+// per quarter of its stages.  Without it the SIMD's oldest-first issue arbitration runs the oldest of its
+// (at most 4) resident waves far ahead of the youngest (measured: the ranks finish at 0.88 / 1.39 / 1.95
+// / 2.49 ms of a 2.5 ms launch), so the launch ends with one wave per SIMD and few loads in flight.  With
+// the bands the lagging waves win arbitration, all finish together, and the launch is 6% shorter.
+// The stage index is wave-uniform: these are scalar compares and s_setprio, no VALU.
+__device__ __forceinline__ void prio_start() { __builtin_amdgcn_s_setprio(3); }
+__device__ __forceinline__ void prio_band(int done, int T) {
+    if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
+    else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
+    else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
+}
 __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "v"(v.y)); }
 
 // element index of (t, component-group p of P, lane) in a time-major SoA stream
@@ -100,8 +156,8 @@ __device__ __forceinline__ double xcost(const double* w, double n0, double n1, d
 //   u_new_t = u_t + K_t (x_new_t - x_t) + gamma sigma_t ;  x_new_{t+1} = RK4(x_new_t, u_new_t)
 // FULLK = false: open loop, u_new_t = u_t.  x pairs (N,2,Bp); u, sigma planes (T,2,Bp); K pairs (T,4,Bp).
 // ------------------------------------------------------------------------------------------
-template <bool FULLK>
-__device__ __forceinline__ double rollout_ref(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+template <bool FULLK, bool WRITE = true>
+__device__ __forceinline__ double rollout_ref(const Dyn& m, const KW& w, const double2* __restrict__ x,
                                               const double* __restrict__ u, const double2* __restrict__ K,
                                               const double* __restrict__ s, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ xn,
@@ -109,8 +165,10 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const gym_weights& w
                                               double n0, double n1, double n2, double n3) {
     const int T = N - 1;
     double J = 0.0;
-    xn[l] = make_double2(n0, n1);
-    xn[Bp + l] = make_double2(n2, n3);
+    if (WRITE) {
+        xn[l] = make_double2(n0, n1);
+        xn[Bp + l] = make_double2(n2, n3);
+    }
     for (int t = 0; t < T; ++t) {
         double v0 = u[pix(t, 0, 2, l, Bp)], v1 = u[pix(t, 1, 2, l, Bp)];
         if (FULLK) {
@@ -122,16 +180,20 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const gym_weights& w
             const double kd1 = ((k2.x * d0 + k2.y * d1) + k3.x * d2) + k3.y * d3;
             v0 = (v0 + kd0) + gamma * s[pix(t, 0, 2, l, Bp)];
             v1 = (v1 + kd1) + gamma * s[pix(t, 1, 2, l, Bp)];
-            un[pix(t, 0, 2, l, Bp)] = v0;
-            un[pix(t, 1, 2, l, Bp)] = v1;
+            if (WRITE) {
+                un[pix(t, 0, 2, l, Bp)] = v0;
+                un[pix(t, 1, 2, l, Bp)] = v1;
+            }
         }
         const double* urt = ur + 2 * t;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
         J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
         J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
         gym::rk4(m, n0, n1, n2, n3, v1);
-        xn[pix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
-        xn[pix(t + 1, 1, 2, l, Bp)] = make_double2(n2, n3);
+        if (WRITE) {
+            xn[pix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
+            xn[pix(t + 1, 1, 2, l, Bp)] = make_double2(n2, n3);
+        }
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
 }
@@ -148,15 +210,15 @@ struct TrialStage {
     double u0;           // tau1 control (0 when U0Z)
 };
 
-template <bool WRITE, bool U0Z>
-__device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights& w, const double* __restrict__ u,
+template <bool WRITE, bool U0Z, bool CK = false, int CP = kNT>
+__device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const double* __restrict__ u,
                                                 const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                 const double* __restrict__ xr, const double* __restrict__ ur,
                                                 double2* __restrict__ xn, double* __restrict__ un, double gamma,
                                                 int64_t l, int64_t Bp, int N, double n0, double n1, double n2,
                                                 double n3) {
     const int T = N - 1;
-    const double G00 = 2.0 * w.R[0], iG00 = 1.0 / G00;
+    const double G00 = w.G00, iG00 = w.iG00;
     const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;   // lane byte offsets (pairs, planes)
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Kb = reinterpret_cast<const char*>(K1);   // stage stride 2 rows
@@ -172,15 +234,17 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights&
     }
     auto fetch = [&](TrialStage& q, int t) {   // stage t's streams into register set q
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        q.k0 = bld2(rK, o2, 0);
-        q.k1 = bld2(rK, o2, row);
-        q.c = bld2(rsrc(Cb + (int64_t)t * row), o2, 0);
-        q.u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
+        q.k0 = bld2<CP>(rK, o2, 0);
+        q.k1 = bld2<CP>(rK, o2, row);
+        q.c = bld2<CP>(rsrc(Cb + (int64_t)t * row), o2, 0);
+        q.u0 = U0Z ? 0.0 : bld1<CP>(rsrc(Ub + (int64_t)t * row), o1, 0);
     };
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
     fetch(pre, 0);
     pin(pre.k0); pin(pre.k1); pin(pre.c); pin(pre.u0);
+    prio_start();
     for (int t = 0; t < T; ++t) {
+        prio_band(t, T);
         const double2 k0 = pre.k0, k1 = pre.k1, c = pre.c;
         const double u0 = pre.u0;
         if (t + 1 < T) fetch(pre, t + 1);
@@ -198,7 +262,7 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const gym_weights&
             bst1(rO, o1, plane, v1);
         }
         gym::rk4(m, n0, n1, n2, n3, v1);
-        if (WRITE) {
+        if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
             bst2(rX, o2, 0, n0, n1);
             bst2(rX, o2, row, n2, n3);
@@ -219,21 +283,18 @@ struct Sweep {
     double P00, P01, P02, P03, P11, P12, P13, P22, P23, P33, p0, p1, p2, p3;
     double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     double dJ = 0.0, smax = 0.0;
-    double twoQ0, twoQ1, twoQ2, twoQ3, G00, twoR1, iG00;
 
     // terminal conditions from x_N (P = 2 Q_T, p = 2 Q_T dx_N; lambda_N = p)
-    __device__ __forceinline__ Sweep(const gym_weights& w, double2 xa, double2 xb, const double* xrT) {
+    __device__ __forceinline__ Sweep(const KW& w, double2 xa, double2 xb, const double* xrT) {
         P00 = 2.0 * w.QT[0]; P11 = 2.0 * w.QT[1]; P22 = 2.0 * w.QT[2]; P33 = 2.0 * w.QT[3];
         P01 = P02 = P03 = P12 = P13 = P23 = 0.0;
         p0 = P00 * (xa.x - xrT[0]); p1 = P11 * (xa.y - xrT[1]);
         p2 = P22 * (xb.x - xrT[2]); p3 = P33 * (xb.y - xrT[3]);
         if (LAMBDA) { l0 = p0; l1 = p1; l2 = p2; l3 = p3; }
-        twoQ0 = 2.0 * w.Q[0]; twoQ1 = 2.0 * w.Q[1]; twoQ2 = 2.0 * w.Q[2]; twoQ3 = 2.0 * w.Q[3];
-        G00 = 2.0 * w.R[0]; twoR1 = 2.0 * w.R[1]; iG00 = 1.0 / G00;
     }
 
     // stage t (x_t = (xa, xb), u_t = (ut0, ut1)): gain row 1 k[0..3], sigma (s0, s1); updates P, p, dJ, smax
-    __device__ __forceinline__ void step(const Dyn& m, double2 xa, double2 xb, double ut0, double ut1,
+    __device__ __forceinline__ void step(const Dyn& m, const KW& w, double2 xa, double2 xb, double ut0, double ut1,
                                          const double* xrt, const double* urt, double& k0, double& k1,
                                          double& k2, double& k3, double& s0, double& s1) {
         const double dt = m.h;
@@ -242,9 +303,9 @@ struct Sweep {
         const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
         const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
         const double bd2 = dt * J.bc2, bd3 = dt * J.bc3;
-        const double q0 = twoQ0 * (xa.x - xrt[0]), q1 = twoQ1 * (xa.y - xrt[1]);
-        const double q2 = twoQ2 * (xb.x - xrt[2]), q3 = twoQ3 * (xb.y - xrt[3]);
-        const double r0 = G00 * (ut0 - urt[0]), r1 = twoR1 * (ut1 - urt[1]);
+        const double q0 = w.twoQ[0] * (xa.x - xrt[0]), q1 = w.twoQ[1] * (xa.y - xrt[1]);
+        const double q2 = w.twoQ[2] * (xb.x - xrt[2]), q3 = w.twoQ[3] * (xb.y - xrt[3]);
+        const double r0 = w.G00 * (ut0 - urt[0]), r1 = w.twoR1 * (ut1 - urt[1]);
         if (LAMBDA) {  // lambda_t = 2Q dx_t + A_d^T lambda_{t+1}
             const double n0 = q0 + (l0 + A20 * l2 + A30 * l3);
             const double n1 = q1 + (l1 + A21 * l2 + A31 * l3);
@@ -255,7 +316,7 @@ struct Sweep {
         // Pb = P B_d[:,1]
         const double Pb0 = P02 * bd2 + P03 * bd3, Pb1 = P12 * bd2 + P13 * bd3;
         const double Pb2 = P22 * bd2 + P23 * bd3, Pb3 = P23 * bd2 + P33 * bd3;
-        const double G11 = twoR1 + (bd2 * Pb2 + bd3 * Pb3);
+        const double G11 = w.twoR1 + (bd2 * Pb2 + bd3 * Pb3);
         // F row 1 = (P b)^T A_d
         const double F0 = Pb0 + A20 * Pb2 + A30 * Pb3;
         const double F1 = Pb1 + A21 * Pb2 + A31 * Pb3;
@@ -264,7 +325,7 @@ struct Sweep {
         const double g1 = r1 + (bd2 * p2 + bd3 * p3);
         const double iG = 1.0 / G11;
         k0 = -F0 * iG; k1 = -F1 * iG; k2 = -F2 * iG; k3 = -F3 * iG;
-        s0 = -r0 * iG00; s1 = -g1 * iG;
+        s0 = -r0 * w.iG00; s1 = -g1 * iG;
         dJ += r0 * s0 + g1 * s1;
         // W = P A_d
         const double W00 = P00 + P02 * A20 + P03 * A30, W01 = P01 + P02 * A21 + P03 * A31;
@@ -277,16 +338,16 @@ struct Sweep {
         const double W32 = dt * P03 + P23 * A22 + P33 * A32, W33 = dt * P13 + P23 * A23 + P33 * A33;
         // P <- 2Q + A_d^T W - K^T G K   (K^T G K = G11 k k^T)
         const double gk0 = G11 * k0, gk1 = G11 * k1, gk2 = G11 * k2, gk3 = G11 * k3;
-        const double nP00 = twoQ0 + (W00 + A20 * W20 + A30 * W30) - gk0 * k0;
+        const double nP00 = w.twoQ[0] + (W00 + A20 * W20 + A30 * W30) - gk0 * k0;
         const double nP01 = (W01 + A20 * W21 + A30 * W31) - gk0 * k1;
         const double nP02 = (W02 + A20 * W22 + A30 * W32) - gk0 * k2;
         const double nP03 = (W03 + A20 * W23 + A30 * W33) - gk0 * k3;
-        const double nP11 = twoQ1 + (W11 + A21 * W21 + A31 * W31) - gk1 * k1;
+        const double nP11 = w.twoQ[1] + (W11 + A21 * W21 + A31 * W31) - gk1 * k1;
         const double nP12 = (W12 + A21 * W22 + A31 * W32) - gk1 * k2;
         const double nP13 = (W13 + A21 * W23 + A31 * W33) - gk1 * k3;
-        const double nP22 = twoQ2 + (dt * W02 + A22 * W22 + A32 * W32) - gk2 * k2;
+        const double nP22 = w.twoQ[2] + (dt * W02 + A22 * W22 + A32 * W32) - gk2 * k2;
         const double nP23 = (dt * W03 + A22 * W23 + A32 * W33) - gk2 * k3;
-        const double nP33 = twoQ3 + (dt * W13 + A23 * W23 + A33 * W33) - gk3 * k3;
+        const double nP33 = w.twoQ[3] + (dt * W13 + A23 * W23 + A33 * W33) - gk3 * k3;
         // p <- q + A_d^T p - K^T G sigma
         const double gs = G11 * s1;
         const double np0 = q0 + (p0 + A20 * p2 + A30 * p3) - k0 * gs;
@@ -302,7 +363,7 @@ struct Sweep {
 
 // API form: writes K row 1 (pairs), sigma planes and optionally lambda; register prefetch of stage t-1.
 template <bool LAMBDA>
-__device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+__device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const double2* __restrict__ x,
                                               const double* __restrict__ u, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ K1,
                                               double* __restrict__ sig, double2* __restrict__ lam, int64_t l,
@@ -325,7 +386,7 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
             pu1 = u[pix(t - 1, 1, 2, l, Bp)];
         }
         double k0, k1, k2, k3, s0, s1;
-        S.step(m, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        S.step(m, w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
         if (LAMBDA) {
             lam[pix(t, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
             lam[pix(t, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
@@ -343,7 +404,7 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const gym_weights& w
 // streams while stage t computes.  U0Z: the tau1 channel is identically zero (u0 = ur0 = 0,
 // GYM_FLAG_U0_ZERO) and its plane is not read.
 template <bool U0Z>
-__device__ __forceinline__ void backward_solver_lane(const Dyn& m, const gym_weights& w,
+__device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
                                                      const double2* __restrict__ x, const double* __restrict__ u,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
                                                      double2* __restrict__ K1, double2* __restrict__ cs, int64_t l,
@@ -364,7 +425,9 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const gym_wei
         if (!U0Z) pu0 = bld1(rU, o1, 0);
     }
     pin(pa); pin(pb); pin(pu0); pin(pu1);
+    prio_start();
     for (int t = T - 1; t >= 0; --t) {
+        prio_band(T - 1 - t, T);
         const double2 xa = pa, xb = pb;
         const double ut0 = pu0, ut1 = pu1;
         if (t > 0) {
@@ -376,7 +439,8 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const gym_wei
             pu1 = bld1(rU, o1, plane);
         }
         double k0, k1, k2, k3, s0, s1;
-        S.step(m, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
+        S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         bst2(rK, o2, 0, k0, k1);
@@ -387,10 +451,112 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const gym_wei
     smax_out = S.smax;
 }
 
+// Checkpointed solver sweep (GYM_FLAG_X_CKPT): the trial stored x only at the knots c0 = 0, CKI, 2 CKI, ...
+// and T.  Going backward one block [c0, c0 + len) at a time, the sweep takes the block's checkpoint x_c0
+// and controls, re-integrates x_{c0+1} .. x_{c0+len-1} with the trial's RK4 (same inputs, same code: the
+// same bits) into a lane-private LDS slot, then runs the block's stages t = c0+len-1 .. c0 from it.  The
+// earlier block's streams are requested after the re-integration, so they land while the block's
+// Riccati stages compute and the prefetch registers are not live across the RK4 (128-VGPR budget).
+// lds: this wavefront's CKI x 2 rows of 64 double2 (knot c0 + j in rows 2j, 2j+1), then CKI rows of 64
+// tau2 controls and (unless U0Z) CKI rows of tau1 controls.
+struct CkBlock {
+    double2 a, b;          // checkpoint x_c0
+    double u0[CKI], u1[CKI];
+};
+
+template <bool U0Z>
+__device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& w,
+                                                        const double2* __restrict__ x, const double* __restrict__ u,
+                                                        const double* __restrict__ xr, const double* __restrict__ ur,
+                                                        double2* __restrict__ K1, double2* __restrict__ cs,
+                                                        double2* __restrict__ lds, int64_t l, int64_t Bp, int N,
+                                                        double& dJ_out, double& smax_out) {
+    const int T = N - 1;
+    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Xb = reinterpret_cast<const char*>(x);
+    const char* Ub = reinterpret_cast<const char*>(u);
+    const char* Kb = reinterpret_cast<const char*>(K1);
+    const char* Cb = reinterpret_cast<const char*>(cs);
+    const int ln = threadIdx.x;
+    double* lu1 = reinterpret_cast<double*>(lds + 2 * CKI * BLK);   // (CKI, 64) tau2 controls
+    double* lu0 = lu1 + CKI * BLK;                                   // (CKI, 64) tau1 controls (!U0Z)
+    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    auto fetch = [&](CkBlock& q, int c0, int len) {
+        const auto rX = rsrc(Xb + (int64_t)c0 * (2 * (int64_t)row));
+        q.a = bld2(rX, o2, 0);
+        q.b = bld2(rX, o2, row);
+#pragma unroll
+        for (int j = 0; j < CKI; ++j) {
+            q.u0[j] = 0.0;
+            q.u1[j] = 0.0;
+            if (j < len) {
+                const auto rU = rsrc(Ub + (int64_t)(c0 + j) * row);
+                if (!U0Z) q.u0[j] = bld1(rU, o1, 0);
+                q.u1[j] = bld1(rU, o1, plane);
+            }
+        }
+    };
+    const int nblk = (T + CKI - 1) / CKI;
+    CkBlock q;
+    {
+        const int c0 = (nblk - 1) * CKI;
+        fetch(q, c0, T - c0);
+    }
+    prio_start();
+    for (int bk = nblk - 1; bk >= 0; --bk) {
+        const int c0 = bk * CKI;
+        const int len = (T - c0 < CKI) ? T - c0 : CKI;
+        prio_band(T - c0 - len, T);
+        // knots c0 .. c0+len-1 into LDS: the checkpoint, then the trial's x_{t+1} = RK4(x_t, u1_t); the
+        // block's controls too, so that no register holds them across the stages
+        {
+            double n0 = q.a.x, n1 = q.a.y, n2 = q.b.x, n3 = q.b.y;
+            lds[ln] = q.a;
+            lds[BLK + ln] = q.b;
+#pragma unroll
+            for (int j = 0; j < CKI; ++j) {
+                lu1[j * BLK + ln] = q.u1[j];
+                if (!U0Z) lu0[j * BLK + ln] = q.u0[j];
+            }
+#pragma unroll
+            for (int j = 0; j < CKI - 1; ++j) {
+                if (j < len - 1) {
+                    gym::rk4(m, n0, n1, n2, n3, q.u1[j]);
+                    lds[(2 * j + 2) * BLK + ln] = make_double2(n0, n1);
+                    lds[(2 * j + 3) * BLK + ln] = make_double2(n2, n3);
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps apart (register pressure)
+            }
+        }
+        if (bk > 0) fetch(q, c0 - CKI, CKI);   // the earlier block (always full) lands during the stages below
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = CKI - 1; j >= 0; --j) {
+            if (j < len) {
+                const int t = c0 + j;
+                const double2 xa = lds[(2 * j) * BLK + ln], xb = lds[(2 * j + 1) * BLK + ln];
+                const double ut1 = lu1[j * BLK + ln], ut0 = U0Z ? 0.0 : lu0[j * BLK + ln];
+                double k0, k1, k2, k3, s0, s1;
+                const KArgs ka = kernarg_consts();
+                S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+                const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
+                const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+                bst2(rK, o2, 0, k0, k1);
+                bst2(rK, o2, row, k2, k3);
+                bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
 // ------------------------------------------------------------------------------------------
 // kernels: API primitives
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights w, const double2* __restrict__ x,
+__global__ __launch_bounds__(BLK) void k_backward_api(Dyn m, KW w, const double2* __restrict__ x,
                                                       const double* __restrict__ u, const double* __restrict__ xr,
                                                       const double* __restrict__ ur, double2* __restrict__ K1,
                                                       double* __restrict__ sig, double* __restrict__ dJ,
@@ -398,7 +564,6 @@ __global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights 
                                                       int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
-    const Dyn m(mm);
     double d, s;
     if (lam)
         backward_lane<true>(m, w, x, u, xr, ur, K1, sig, lam, l, Bp, N, d, s);
@@ -408,19 +573,18 @@ __global__ __launch_bounds__(BLK) void k_backward_api(gym_model mm, gym_weights 
     if (smax) smax[l] = s;
 }
 
-__global__ __launch_bounds__(BLK) void k_open_loop(gym_model mm, gym_weights w, const double* __restrict__ x0,
+__global__ __launch_bounds__(BLK) void k_open_loop(Dyn m, KW w, const double* __restrict__ x0,
                                                    const double* __restrict__ u, const double* __restrict__ xr,
                                                    const double* __restrict__ ur, double2* __restrict__ xn,
                                                    double* __restrict__ cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
-    const Dyn m(mm);
     const double J = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
                                         x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
     if (cost) cost[l] = J;
 }
 
-__global__ __launch_bounds__(BLK) void k_closed_loop(gym_model mm, gym_weights w, const double2* __restrict__ x,
+__global__ __launch_bounds__(BLK) void k_closed_loop(Dyn m, KW w, const double2* __restrict__ x,
                                                      const double* __restrict__ u, const double2* __restrict__ Kf,
                                                      const double* __restrict__ s, const double* __restrict__ gamma,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
@@ -428,17 +592,15 @@ __global__ __launch_bounds__(BLK) void k_closed_loop(gym_model mm, gym_weights w
                                                      double* __restrict__ cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
-    const Dyn m(mm);
     const double2 a = x[l], b = x[Bp + l];
     const double J = rollout_ref<true>(m, w, x, u, Kf, s, xr, ur, xn, un, gamma[l], l, Bp, N, a.x, a.y, b.x, b.y);
     if (cost) cost[l] = J;
 }
 
-__global__ void k_point(gym_model mm, const double* __restrict__ x, const double* __restrict__ u,
+__global__ void k_point(Dyn m, const double* __restrict__ x, const double* __restrict__ u,
                         double* __restrict__ out, double* __restrict__ out2, int64_t n, int what) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const Dyn m(mm);
     double x0 = x[4 * i], x1 = x[4 * i + 1], x2 = x[4 * i + 2], x3 = x[4 * i + 3];
     const double tau2 = u[2 * i + 1];  // tau1 is not an acrobot input (dynamics.py:205, :153)
     if (what == 0) {                   // continuous_dynamics
@@ -526,7 +688,7 @@ __global__ __launch_bounds__(BLK) void k_total_cost(const double2* __restrict__ 
 }
 
 // build_stage_lists (:166-181) as plain-double SoA for the generic Riccati path
-__global__ __launch_bounds__(BLK) void k_linearize(gym_model mm, gym_weights w, const double2* __restrict__ x,
+__global__ __launch_bounds__(BLK) void k_linearize(Dyn m, KW w, const double2* __restrict__ x,
                                                    const double* __restrict__ u, const double* __restrict__ xr,
                                                    const double* __restrict__ ur, double* __restrict__ Ad,
                                                    double* __restrict__ Bd, double* __restrict__ q,
@@ -534,7 +696,6 @@ __global__ __launch_bounds__(BLK) void k_linearize(gym_model mm, gym_weights w, 
                                                    int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
-    const Dyn m(mm);
     const double dt = m.h;
     const int T = N - 1;
     for (int t = 0; t < T; ++t) {
@@ -734,7 +895,7 @@ __global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restric
 // ------------------------------------------------------------------------------------------
 // kernels: batched Newton / Armijo solver (newton_Algorithm :298-398)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const double* __restrict__ x0,
+__global__ __launch_bounds__(BLK) void k_init(Dyn m, KW w, const double* __restrict__ x0,
                                               const double* __restrict__ u, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ xn,
                                               double* __restrict__ cost, int32_t* __restrict__ status,
@@ -751,7 +912,6 @@ __global__ __launch_bounds__(BLK) void k_init(gym_model mm, gym_weights w, const
         return;
     }
     status[l] = GYM_ACTIVE;
-    const Dyn m(mm);
     cost[l] = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
                                  x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
 }
@@ -779,28 +939,36 @@ struct WaveTrace {
 #define GYM_TRACE_WAVE(k)
 #endif
 
+// lane-private LDS of the checkpointed sweep: CKI knots x 2 pairs + CKI controls (tau2; and tau1 unless
+// U0Z) x 64 lanes: 10 KiB per wave with U0Z, so 16 waves fill one CU's 160 KiB exactly.
+constexpr int ck_lds_doubles(bool ck, bool u0z) { return ck ? (4 + (u0z ? 1 : 2)) * CKI * BLK : 2; }
+#define GYM_CK_LDS(CK, U0Z) __shared__ double2 ck_lds[ck_lds_doubles(CK, U0Z) / 2]
+
 // Lane ranges: the serial schedule runs every lane [0, B); the pipelined schedule splits the batch
 // into two halves H0 = [0, Bh), H1 = [Bh, B) whose iterations are offset by one phase.
 struct Range {
     int64_t lo, hi;
 };
 
-template <bool U0Z>
-__device__ __forceinline__ void backward_solver(const Dyn& m, const gym_weights& w, const double2* __restrict__ x,
+template <bool U0Z, bool CK>
+__device__ __forceinline__ void backward_solver(const Dyn& m, const KW& w, const double2* __restrict__ x,
                                                 const double* __restrict__ u, const double* __restrict__ xr,
                                                 const double* __restrict__ ur, double2* __restrict__ K1,
                                                 double2* __restrict__ cs, double* __restrict__ dJ,
                                                 double* __restrict__ smax, double* __restrict__ hist_smax, int64_t l,
-                                                int64_t Bp, int N, int k, int hist_len) {
+                                                int64_t Bp, int N, int k, int hist_len, double2* __restrict__ lds) {
     double d, s;
-    backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
+    if (CK)
+        backward_solver_lane_ck<U0Z>(m, w, x, u, xr, ur, K1, cs, lds, l, Bp, N, d, s);
+    else
+        backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
 }
 
-template <bool U0Z>
-__global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weights w, const double2* __restrict__ x,
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK, 4) void k_nt_backward(Dyn m, KW w, const double2* __restrict__ x,
                                                         const double* __restrict__ u, const double* __restrict__ xr,
                                                         const double* __restrict__ ur, double2* __restrict__ K1,
                                                         double2* __restrict__ cs, double* __restrict__ dJ,
@@ -810,9 +978,9 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_backward(gym_model mm, gym_weight
                                                         int k, int hist_len) {
     GYM_TRACE_WAVE(0);
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
+    GYM_CK_LDS(CK, U0Z);
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
-    const Dyn m(mm);
-    backward_solver<U0Z>(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len);
+    backward_solver<U0Z, CK>(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len, ck_lds);
 }
 
 struct SolverCtl {
@@ -846,8 +1014,8 @@ struct TrialIO {
 };
 
 // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass).
-template <bool U0Z>
-__device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w, const SolverCtl& a, const TrialIO& io,
+template <bool U0Z, bool CK>
+__device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const SolverCtl& a, const TrialIO& io,
                                              const double2* __restrict__ K1, const double2* __restrict__ cs,
                                              const double* __restrict__ xr, const double* __restrict__ ur,
                                              double* __restrict__ cost, const double* __restrict__ dJ,
@@ -858,8 +1026,8 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w,
                                              double* __restrict__ hist_cost, int64_t l, int64_t Bp, int N) {
     const double2 xa = io.x[l], xb = io.x[Bp + l];
     const double g = a.gamma0;
-    const double Jn = rollout_cform<true, U0Z>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y,
-                                               xb.x, xb.y);
+    const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
+                                                   xa.y, xb.x, xb.y);
     n_roll[l] += 1;
     if (Jn < cost[l] + a.c * g * dJ[l]) {  // strict Armijo test (:361)
         n_iter[l] += 1;
@@ -872,8 +1040,8 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const gym_weights& w,
     }
 }
 
-template <bool U0Z>
-__global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK, 4) void k_nt_trial(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                      const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
                                                      double* __restrict__ cost, const double* __restrict__ dJ,
@@ -884,17 +1052,16 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_trial(gym_model mm, gym_weights w
                                                      double* __restrict__ hist_cost, Range rg, int64_t Bp, int N) {
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
-    const Dyn m(mm);
     GYM_TRACE_WAVE(1);
-    trial_solver<U0Z>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+    trial_solver<U0Z, CK>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
                       retry_list + rg.lo, counter, hist_cost, l, Bp, N);
 }
 
 // One pipeline phase: the first nb_b workgroups run the backward sweep of one half, the rest run the
 // Armijo trial of the other half.  The sweep is HBM-bound and the trial fp64-VALU-bound, so co-resident
 // waves of the two kinds overlap memory and arithmetic on every CU.  The two halves' lanes are disjoint.
-template <bool U0Z>
-__global__ __launch_bounds__(BLK, 4) void k_nt_phase(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK, 4) void k_nt_phase(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                      const double2* __restrict__ xb_in,
                                                      const double* __restrict__ ub_in, int kb, int nb_b,
                                                      Range rb, Range rt, double2* __restrict__ K1,
@@ -906,22 +1073,23 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(gym_model mm, gym_weights w
                                                      int32_t* __restrict__ n_roll, int32_t* __restrict__ retry_list,
                                                      int32_t* __restrict__ counter, double* __restrict__ hist_cost,
                                                      double* __restrict__ hist_smax, int64_t Bp, int N) {
-    const Dyn m(mm);
+    GYM_CK_LDS(CK, U0Z);
     if ((int)blockIdx.x < nb_b) {
         const int64_t l = rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
         if (l >= rb.hi || status[l] != GYM_ACTIVE) return;
-        backward_solver<U0Z>(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len);
+        backward_solver<U0Z, CK>(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len,
+                                 ck_lds);
     } else {
         const int64_t l = rt.lo + (int64_t)(blockIdx.x - nb_b) * BLK + threadIdx.x;
         if (l >= rt.hi || status[l] != GYM_ACTIVE) return;
-        trial_solver<U0Z>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
-                          retry_list + rt.lo, counter, hist_cost, l, Bp, N);
+        trial_solver<U0Z, CK>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+                              retry_list + rt.lo, counter, hist_cost, l, Bp, N);
     }
 }
 
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
 template <bool U0Z>
-__global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+__global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                        const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                        const double* __restrict__ xr, const double* __restrict__ ur,
                                                        const double* __restrict__ cost, const double* __restrict__ dJ,
@@ -930,7 +1098,6 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights
                                                        uint8_t* __restrict__ cand_ok, int64_t Bp, int N) {
     const int nj = a.max_ls - 1;
     const int64_t total = (int64_t)(*counter) * nj;
-    const Dyn m(mm);
     for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
         const int64_t r = i / nj;
         const int j = 1 + (int)(i % nj);
@@ -945,8 +1112,8 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(gym_model mm, gym_weights
 }
 
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
-template <bool U0Z>
-__global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, SolverCtl a, TrialIO io,
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                   const double2* __restrict__ K1, const double2* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
                                                   double* __restrict__ cost, const double* __restrict__ smax,
@@ -958,7 +1125,6 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, S
                                                   int64_t Bp, int N) {
     const int nr = *counter;
     const int nj = a.max_ls - 1;
-    const Dyn m(mm);
     for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < nr; i += (int64_t)gridDim.x * BLK) {
         const int64_t l = retry_list[i];
         int jacc = 0;
@@ -974,10 +1140,67 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(gym_model mm, gym_weights w, S
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
         const double2 xa = io.x[l], xb = io.x[Bp + l];
-        const double Jn = rollout_cform<true, U0Z>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x, xa.y,
-                                                   xb.x, xb.y);
+        const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
+                                                       xa.y, xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Armijo gamma sweeps (plot_armijo_line_search :254-265): J(gamma_g) of the candidate rollout for G step
+// sizes per lane, cost only, one thread per (lane, g).  The G blocks of one lane group re-read the same
+// streams, so a group's blocks are mapped onto one XCD (blocks are dealt round-robin over the 8 XCDs) and
+// run back to back there: the re-reads hit that XCD's L2.  gridDim.x is a multiple of 8.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool sweep_block(int G, int64_t groups, int64_t& grp, int& g) {
+    const int64_t per = gridDim.x / 8;
+    const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    grp = i / G;
+    g = (int)(i % G);
+    return grp < groups;
+}
+
+// reference form: full gains Kf (T,4,Bp), sigma planes, u_new = u + K (x_new - x) + gamma sigma
+__global__ __launch_bounds__(BLK) void k_gamma_sweep(Dyn m, KW w, const double2* __restrict__ x,
+                                                     const double* __restrict__ u, const double2* __restrict__ Kf,
+                                                     const double* __restrict__ sig, const double* __restrict__ gammas,
+                                                     int G, const double* __restrict__ xr,
+                                                     const double* __restrict__ ur, double* __restrict__ cost_out,
+                                                     int64_t B, int64_t Bp, int N) {
+    int64_t grp;
+    int g;
+    if (!sweep_block(G, Bp / BLK, grp, g)) return;
+    const int64_t l = grp * BLK + threadIdx.x;
+    if (l >= B) {
+        cost_out[(int64_t)g * Bp + l] = __builtin_nan("");
+        return;
+    }
+    const double2 a = x[l], b = x[Bp + l];
+    cost_out[(int64_t)g * Bp + l] = rollout_ref<true, false>(m, w, x, u, Kf, sig, xr, ur, nullptr, nullptr, gammas[g],
+                                                             l, Bp, N, a.x, a.y, b.x, b.y);
+}
+
+// solver form: the Armijo trial's own rollout (offset form) on a batch's iteration-k streams; at the
+// trial's step sizes the costs are bit-identical to the trial's.  Non-active lanes get NaN.
+template <bool U0Z>
+__global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const double2* __restrict__ x,
+                                                        const double* __restrict__ u, const double2* __restrict__ K1,
+                                                        const double2* __restrict__ cs,
+                                                        const double* __restrict__ gammas, int G,
+                                                        const double* __restrict__ xr, const double* __restrict__ ur,
+                                                        const int32_t* __restrict__ status,
+                                                        double* __restrict__ cost_out, int64_t B, int64_t Bp, int N) {
+    int64_t grp;
+    int g;
+    if (!sweep_block(G, Bp / BLK, grp, g)) return;
+    const int64_t l = grp * BLK + threadIdx.x;
+    if (l >= B || status[l] != GYM_ACTIVE) {
+        cost_out[(int64_t)g * Bp + l] = __builtin_nan("");
+        return;
+    }
+    const double2 a = x[l], b = x[Bp + l];
+    cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, false, 0>(m, w, u, K1, cs, xr, ur, nullptr, nullptr,
+                                                                        gammas[g], l, Bp, N, a.x, a.y, b.x, b.y);
 }
 
 // Deterministic two-stage statistics reduction (fixed lane->thread map, fixed trees).
@@ -1055,7 +1278,7 @@ __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restr
 
 // sigma of each lane's last iteration, lane-major (B,T,2): sigma1 from the sweep's (c1, sigma1) stream,
 // sigma0 = -(2R0 (u0 - ur0)) / (2R0) recomputed from that iteration's controls, buffer (n_iter-1) & 1.
-__global__ void k_finalize_sigma(gym_weights w, const double2* __restrict__ cs, const double* __restrict__ u0b,
+__global__ void k_finalize_sigma(KW w, const double2* __restrict__ cs, const double* __restrict__ u0b,
                                  const double* __restrict__ u1b, const double* __restrict__ ur,
                                  const int32_t* __restrict__ n_iter, double* __restrict__ sig, int64_t B, int64_t Bp,
                                  int T) {
@@ -1067,12 +1290,32 @@ __global__ void k_finalize_sigma(gym_weights w, const double2* __restrict__ cs, 
     double s0 = 0.0, s1 = 0.0;
     if (it > 0) {
         const double* u = ((it - 1) & 1) ? u1b : u0b;
-        const double G00 = 2.0 * w.R[0];
-        s0 = -(G00 * (u[pix(t, 0, 2, lane, Bp)] - ur[2 * t])) * (1.0 / G00);
+        s0 = -(w.G00 * (u[pix(t, 0, 2, lane, Bp)] - ur[2 * t])) * w.iG00;
         s1 = cs[(int64_t)t * Bp + lane].y;
     }
     sig[2 * o] = s0;
     sig[2 * o + 1] = s1;
+}
+
+// GYM_FLAG_X_CKPT: rebuild every knot of a state buffer from x_0 and the tau2 controls, x_{t+1} =
+// RK4(x_t, u1_t) -- the same recursion (and code) the trial ran, so the rebuilt knots equal the bits it
+// would have stored and the checkpoints are rewritten unchanged.  sel_buf < 0: lane l's res_buf.
+__global__ __launch_bounds__(BLK) void k_fill_states(Dyn m, double2* __restrict__ x0b, double2* __restrict__ x1b,
+                                                     const double* __restrict__ u0b, const double* __restrict__ u1b,
+                                                     const int32_t* __restrict__ res_buf, int sel_buf, int64_t B,
+                                                     int64_t Bp, int N) {
+    const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
+    if (l >= B) return;
+    const int sel = sel_buf >= 0 ? sel_buf : res_buf[l];
+    double2* xs = sel ? x1b : x0b;
+    const double* us = sel ? u1b : u0b;
+    const double2 a = xs[l], b = xs[Bp + l];
+    double n0 = a.x, n1 = a.y, n2 = b.x, n3 = b.y;
+    for (int t = 0; t < N - 1; ++t) {
+        gym::rk4(m, n0, n1, n2, n3, us[pix(t, 1, 2, l, Bp)]);
+        st_nt(xs + pix(t + 1, 0, 2, l, Bp), n0, n1);
+        st_nt(xs + pix(t + 1, 1, 2, l, Bp), n2, n3);
+    }
 }
 
 struct TimedLaunch {  // records a start/stop event pair around one launch if the slot is free
@@ -1094,6 +1337,10 @@ struct TimedLaunch {  // records a start/stop event pair around one launch if th
 
 // kernel instantiation for the batch's tau1 mode (GYM_FLAG_U0_ZERO)
 #define U0Z_SEL(b, kern) (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true> : kern<false>)
+// ... and its state-checkpointing mode (GYM_FLAG_X_CKPT)
+#define SOLVER_SEL(b, kern)                                                                               \
+    (((b)->flags & GYM_FLAG_U0_ZERO) ? (((b)->flags & GYM_FLAG_X_CKPT) ? kern<true, true> : kern<true, false>) \
+                                     : (((b)->flags & GYM_FLAG_X_CKPT) ? kern<false, true> : kern<false, false>))
 
 inline bool bad_dims(int64_t B, int64_t Bp, int N) {
     return B <= 0 || Bp < B || (Bp % 64) != 0 || Bp > GYM_MAX_BP || N < 2;
@@ -1131,7 +1378,7 @@ static int point_op(const gym_model* m, const double* x, const double* u, double
                     int what) {
     if (!m || !x || !u || !o1 || n < 0 || (what == 2 && !o2)) return GYM_EINVAL;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_point, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, *m, x, u, o1, o2, n, what);
+    hipLaunchKernelGGL(k_point, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, Dyn(*m), x, u, o1, o2, n, what);
     return launch_status();
 }
 
@@ -1185,7 +1432,7 @@ int gym_rollout_open_loop(const gym_model* m, const gym_weights* w, const double
                           const double* xr, const double* ur, double* x, double* cost, int64_t B, int64_t Bp,
                           int32_t N, void* s) {
     if (!m || !w || !x0 || !u || !xr || !ur || !x || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_open_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, x0, u, xr, ur,
+    hipLaunchKernelGGL(k_open_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), kw(*w), x0, u, xr, ur,
                        (double2*)x, cost, B, Bp, N);
     return launch_status();
 }
@@ -1195,7 +1442,7 @@ int gym_closed_loop(const gym_model* m, const gym_weights* w, const double* x, c
                     double* un, double* cost, int64_t B, int64_t Bp, int32_t N, void* s) {
     if (!m || !w || !x || !u || !Kf || !sigma || !gamma || !xr || !ur || !xn || !un || bad_dims(B, Bp, N))
         return GYM_EINVAL;
-    hipLaunchKernelGGL(k_closed_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w,
+    hipLaunchKernelGGL(k_closed_loop, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), kw(*w),
                        (const double2*)x, u, (const double2*)Kf, sigma, gamma, xr, ur, (double2*)xn, un, cost, B, Bp,
                        N);
     return launch_status();
@@ -1213,7 +1460,7 @@ int gym_backward_sweep(const gym_model* m, const gym_weights* w, const double* x
                        const double* ur, double* K1, double* sigma, double* dJ, double* smax, double* lambda, int64_t B,
                        int64_t Bp, int32_t N, void* s) {
     if (!m || !w || !x || !u || !xr || !ur || !K1 || !sigma || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_backward_api, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w,
+    hipLaunchKernelGGL(k_backward_api, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), kw(*w),
                        (const double2*)x, u, xr, ur, (double2*)K1, sigma, dJ, smax, (double2*)lambda, B, Bp, N);
     return launch_status();
 }
@@ -1222,7 +1469,7 @@ int gym_linearize(const gym_model* m, const gym_weights* w, const double* x, con
                   const double* ur, double* Ad, double* Bd, double* q, double* r, double* qT, int64_t B, int64_t Bp,
                   int32_t N, void* s) {
     if (!m || !w || !x || !u || !xr || !ur || !Ad || !Bd || !q || !r || !qT || bad_dims(B, Bp, N)) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_linearize, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, *m, *w, (const double2*)x, u,
+    hipLaunchKernelGGL(k_linearize, dim3(grid_for(B, BLK)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), kw(*w), (const double2*)x, u,
                        xr, ur, Ad, Bd, q, r, qT, B, Bp, N);
     return launch_status();
 }
@@ -1257,7 +1504,7 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(b->stats, 0, sizeof(double) * 24, st);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, *m, *w, x0, b->u[0], b->x_ref, b->u_ref,
+    hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w), x0, b->u[0], b->x_ref, b->u_ref,
                        (double2*)b->x[0], b->cost, b->status, b->n_iter, b->res_buf, b->n_roll, b->gamma, b->smax,
                        b->dJ, b->B, b->Bp, b->N);
     return launch_status();
@@ -1274,11 +1521,11 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
         {
             TimedLaunch tl(b->timing, 2, st);
             const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
-            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref, b->u_ref,
+            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
                                b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, *m, *w, c, io, K1, cs, b->x_ref,
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
                            b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
                            b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
     }
@@ -1307,14 +1554,14 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     const bool hist = a->record_history != 0;
     {
         TimedLaunch tl(b->timing, 0, st);
-        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, *m, *w, io.x, io.u, b->x_ref, b->u_ref,
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
                            (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
                            hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     {
         TimedLaunch tl(b->timing, 1, st);
-        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, *m, *w, c, io, (const double2*)b->K1,
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, (const double2*)b->K1,
                            (const double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
                            all, b->Bp, b->N);
@@ -1350,7 +1597,7 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
     const TrialIO io = trial_io(b, kt < 0 ? 0 : kt);
     if (nb_b + nb_t > 0) {
         TimedLaunch tl(b->timing, (p & 1) ? 5 : 6, st);
-        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, *m, *w, c, io,
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io,
                            (const double2*)b->x[kb & 1], b->u[kb & 1], kb, nb_b, rb, rt, (double2*)b->K1,
                            (double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters + ht,
@@ -1362,15 +1609,24 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
     return launch_status();
 }
 
-int gym_newton_finalize(const gym_weights* w, const gym_batch* b, int32_t k_done, double* x_out, double* u_out,
-                        double* K_out, double* sig_out, void* s) {
-    if (!w || bad_batch(b) || k_done < 0) return GYM_EINVAL;
+int gym_newton_fill_states(const gym_model* m, const gym_batch* b, int32_t buf, void* s) {
+    if (!m || bad_batch(b) || buf < -1 || buf > 1) return GYM_EINVAL;
+    if (!(b->flags & GYM_FLAG_X_CKPT)) return 0;
+    hipLaunchKernelGGL(k_fill_states, dim3(grid_for(b->B, BLK)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), (double2*)b->x[0],
+                       (double2*)b->x[1], b->u[0], b->u[1], b->res_buf, (int)buf, b->B, b->Bp, b->N);
+    return launch_status();
+}
+
+int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batch* b, int32_t k_done, double* x_out,
+                        double* u_out, double* K_out, double* sig_out, void* s) {
+    if (!m || !w || bad_batch(b) || k_done < 0) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     hipLaunchKernelGGL(k_finalize_status, dim3(grid_for(b->B, 256)), dim3(256), 0, st, b->status, b->res_buf, b->B,
                        (int)k_done);
     int e = launch_status();
     if (e) return e;
     const int T = b->N - 1;
+    if (x_out && (e = gym_newton_fill_states(m, b, -1, s))) return e;
     if (x_out && (e = gym_unpack_lanes(b->x[0], b->x[1], b->res_buf, x_out, b->B, b->Bp, b->N, 4, 2, s))) return e;
     if (u_out && (e = gym_unpack_lanes(b->u[0], b->u[1], b->res_buf, u_out, b->B, b->Bp, T, 2, 1, s))) return e;
     if (K_out && (e = gym_unpack_gains(b->K1, K_out, b->B, b->Bp, T, s))) return e;
@@ -1381,8 +1637,43 @@ int gym_newton_finalize(const gym_weights* w, const gym_batch* b, int32_t k_done
 int gym_newton_sigma(const gym_weights* w, const gym_batch* b, double* sig_out, void* s) {
     if (!w || bad_batch(b) || !sig_out) return GYM_EINVAL;
     const int T = b->N - 1;
-    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, (hipStream_t)s, *w,
+    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, (hipStream_t)s, kw(*w),
                        (const double2*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
+    return launch_status();
+}
+
+static int sweep_grid(int64_t Bp, int G) {
+    const int64_t nb = (Bp / BLK) * (int64_t)G;
+    return (int)((nb + 7) / 8 * 8);
+}
+
+int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, const double* u, const double* Kf,
+                    const double* sigma, const double* gammas, int32_t G, const double* xr, const double* ur,
+                    double* cost_out, int64_t B, int64_t Bp, int32_t N, void* s) {
+    if (!m || !w || !x || !u || !Kf || !sigma || !gammas || !xr || !ur || !cost_out || G < 1 || bad_dims(B, Bp, N) ||
+        (Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8)
+        return GYM_EINVAL;
+    hipLaunchKernelGGL(k_gamma_sweep, dim3(sweep_grid(Bp, G)), dim3(BLK), 0, (hipStream_t)s, Dyn(*m), kw(*w),
+                       (const double2*)x, u, (const double2*)Kf, sigma, gammas, (int)G, xr, ur, cost_out, B, Bp, N);
+    return launch_status();
+}
+
+int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_batch* b, int32_t k,
+                           const double* gammas, int32_t G, double* cost_out, void* s) {
+    if (!m || !w || bad_batch(b) || k < 0 || !gammas || !cost_out || G < 1 ||
+        (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8)
+        return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
+    const TrialIO io = trial_io(b, k);
+    // iteration k's backward sweep (K1, cs, dJ, smax: the values iteration k itself computes)
+    hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+                       io.x, io.u, b->x_ref, b->u_ref, (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
+                       (double*)nullptr, Range{0, b->B}, b->Bp, b->N, (int)k, 0);
+    int e = launch_status();
+    if (e) return e;
+    hipLaunchKernelGGL(U0Z_SEL(b, k_nt_gamma_sweep), dim3(sweep_grid(b->Bp, G)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+                       io.x, io.u, (const double2*)b->K1, (const double2*)b->cs, gammas, (int)G, b->x_ref, b->u_ref,
+                       b->status, cost_out, b->B, b->Bp, b->N);
     return launch_status();
 }
 

@@ -158,13 +158,12 @@ __global__ void k_lq_forward(const double* __restrict__ A, const double* __restr
 // Batched closed-loop tracking simulation (simulate_tracking :206-216; MPC loop :43-60):
 //   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
 // x0 (B,4) lane-major; shared x_ff (N,4), u_ff (T,2), K (T,2,4); out x (N,2,Bp) pairs, u (T,2,Bp) planes.
-__global__ __launch_bounds__(64) void k_track_rollout(gym_model mm, const double* __restrict__ x0,
+__global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __restrict__ x0,
                                                       const double* __restrict__ x_ff, const double* __restrict__ u_ff,
                                                       const double* __restrict__ K, int64_t B, int64_t Bp, int N,
                                                       double2* __restrict__ xo, double* __restrict__ uo) {
     const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= B) return;
-    const Dyn m(mm);
     const int T = N - 1;
     double n0 = x0[4 * l], n1 = x0[4 * l + 1], n2 = x0[4 * l + 2], n3 = x0[4 * l + 3];
     xo[l] = make_double2(n0, n1);
@@ -225,7 +224,7 @@ int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, 
     if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || Bp < B || (Bp % 64) != 0 ||
         Bp > GYM_MAX_BP || N < 2)
         return GYM_EINVAL;
-    hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, *m, x0, x_ff,
+    hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, Dyn(*m), x0, x_ff,
                        u_ff, K, B, Bp, N, (double2*)x_out, u_out);
     return launch_status();
 }

@@ -205,6 +205,28 @@ class AcrobotEngine:
                                             self.stream), "gym_closed_loop")
         return self.unpack(xn, B), self.unpack(un, B), J[:B]
 
+    def gamma_sweep(self, x, u, K, sigma, gammas, x_ref, u_ref) -> torch.Tensor:
+        """J(gamma_g) of forward_closed_loop_update + total_cost for each lane and step size (the reference's
+        Armijo line-search curve, plot_armijo_line_search :258-264): x (B,N,4), u (B,T,2), K (B,T,2,4),
+        sigma (B,T,2), gammas (G,) -> (B, G)."""
+        x = self.t(x); u = self.t(u); K = self.t(K); sigma = self.t(sigma)
+        g = self.t(gammas).reshape(-1)
+        B, N, _ = x.shape
+        T = N - 1
+        G = int(g.numel())
+        if G < 1:
+            raise ValueError("gamma_sweep needs at least one step size")
+        x_ref, u_ref = self.refs(x_ref, u_ref)
+        Bp = padded(B)
+        xs, us = self.pack(x, Bp), self.pack(u, Bp, W=1)
+        Ks = self.pack(K.reshape(B, T, 8), Bp)
+        ss = self.pack(sigma, Bp, W=1)
+        J = torch.empty((G, Bp), dtype=F64, device=self.device)
+        _lib.check(self.lib.gym_gamma_sweep(C.byref(self.model), C.byref(self._w), xs.data_ptr(), us.data_ptr(),
+                                            Ks.data_ptr(), ss.data_ptr(), g.data_ptr(), G, x_ref.data_ptr(),
+                                            u_ref.data_ptr(), J.data_ptr(), B, Bp, N, self.stream), "gym_gamma_sweep")
+        return J[:, :B].t()
+
     def total_cost(self, x, u, x_ref, u_ref, Q, R, QT):
         x = self.t(x); u = self.t(u)
         B, N, _ = x.shape

@@ -65,7 +65,7 @@ class BatchedNewtonSolver:
 
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
-                 u0_zero: bool | None = None):
+                 u0_zero: bool | None = None, checkpoint: bool = False):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         self.eng = engine
@@ -106,7 +106,11 @@ class BatchedNewtonSolver:
         if u0_zero and not ref_u0_zero:
             raise ValueError("u0_zero=True requires u_ref[:, 0] == 0")
         self.u0_zero = ref_u0_zero if u0_zero is None else bool(u0_zero)
-        b.flags = _lib.FLAG_U0_ZERO if self.u0_zero else 0
+        # state checkpointing (GYM_FLAG_X_CKPT, opt-in): trials store x at every CKPT_INTERVAL-th knot only
+        # and the sweep re-integrates the rest -- bit-identical results, 48 B/stage less traffic, but +0.75 RK4
+        # per sweep stage: on MI355X the solver is as VALU- as HBM-limited and this measured 13% slower
+        self.checkpoint = bool(checkpoint)
+        b.flags = (_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0)
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
         for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
@@ -191,10 +195,43 @@ class BatchedNewtonSolver:
         u = torch.empty((B, T, 2), dtype=F64, device=dev)
         K = torch.empty((B, T, 2, 4), dtype=F64, device=dev)
         s = torch.empty((B, T, 2), dtype=F64, device=dev)
-        _lib.check(self.eng.lib.gym_newton_finalize(C.byref(self.eng._w), C.byref(self.batch), self.k, x.data_ptr(),
+        _lib.check(self.eng.lib.gym_newton_finalize(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.batch),
+                                                    self.k, x.data_ptr(),
                                                     u.data_ptr(), K.data_ptr(), s.data_ptr(), self.eng.stream),
                    "gym_newton_finalize")
         return x, u, K, s
+
+    def states(self, buf: int) -> torch.Tensor:
+        """Every knot of state buffer ``buf`` (SoA (N,2,Bp,2)), rebuilt from its checkpoints if checkpointing."""
+        _lib.check(self.eng.lib.gym_newton_fill_states(C.byref(self.eng.model), C.byref(self.batch), int(buf),
+                                                       self.eng.stream), "gym_newton_fill_states")
+        return self.x[buf]
+
+    def gamma_sweep(self, gammas) -> torch.Tensor:
+        """Armijo line-search curve of every lane at the current iterate (the one iteration ``self.k`` starts
+        from): J(gamma_g) of the trial rollout along iteration k's direction, (B, G); NaN for finished lanes.
+        At the trial step sizes gamma_0 beta^i the values are the Armijo trials' costs bit for bit.  Runs
+        iteration k's backward sweep, which that iteration recomputes identically, so the solve is unchanged."""
+        g = self.eng.t(gammas).reshape(-1)
+        G = int(g.numel())
+        if G < 1:
+            raise ValueError("gamma_sweep needs at least one step size")
+        J = torch.empty((G, self.Bp), dtype=F64, device=self.eng.device)
+        _lib.check(self.eng.lib.gym_newton_gamma_sweep(C.byref(self.eng.model), C.byref(self.eng._w),
+                                                       C.byref(self.batch), self.k, g.data_ptr(), G, J.data_ptr(),
+                                                       self.eng.stream), "gym_newton_gamma_sweep")
+        return J[:, :self.B].t()
+
+    def gains(self) -> torch.Tensor:
+        """K (B,T,2,4) of every lane's most recent backward sweep."""
+        K = torch.empty((self.B, self.T, 2, 4), dtype=F64, device=self.eng.device)
+        _lib.check(self.eng.lib.gym_unpack_gains(self.K1.data_ptr(), K.data_ptr(), self.B, self.Bp, self.T,
+                                                 self.eng.stream), "gym_unpack_gains")
+        return K
+
+    def controls(self, buf: int) -> torch.Tensor:
+        """u (B,T,2) of control buffer ``buf``."""
+        return self.eng.unpack(self.u[buf], self.B)
 
     def sigma(self) -> torch.Tensor:
         """sigma (B,T,2) of every lane's most recent backward sweep."""

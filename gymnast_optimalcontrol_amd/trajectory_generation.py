@@ -12,6 +12,7 @@ argument order, defaults, return structure and error behaviour:
   calculate_K_and_sigma (:183)      -> gym_riccati_general
   forward_closed_loop_update (:218) -> gym_closed_loop
   total_cost (:231)                 -> gym_total_cost
+  plot_armijo_line_search (:254)    -> gym_gamma_sweep (the 200-rollout curve) + the reference's figure
   newton_Algorithm (:298)           -> gym_newton_init / gym_newton_iteration / gym_newton_finalize
   get_fully_actuated_ref (:511), compute_equilibrium (:22), define_reference_piecewise (:41)
                                     (problem setup on the host, as in the reference)
@@ -173,9 +174,69 @@ def total_cost(x_traj, u_traj, x_ref, u_ref, Q, R, Q_T):
     return float(J[0])
 
 
-def plot_armijo_line_search(*args, **kwargs):
-    """Plotting is out of scope of the accelerated path (reference :254-296); intentionally a no-op."""
-    return None
+def armijo_steps(gamma_0, beta, n):
+    """The Armijo trial step sizes gamma_0, gamma_0 beta, ... as the reference forms them: gamma_i *= beta,
+    sequentially (:365) -- bit-identical to the solver kernels' (beta ** i would round differently)."""
+    g = [float(gamma_0)]
+    for _ in range(n - 1):
+        g.append(g[-1] * beta)
+    return np.array(g)
+
+
+def plot_armijo_line_search(iteration, x_traj, u_traj, K, sigma, cost_current, x_ref, u_ref, delta_J,
+                            gamma_accepted, stepsizes_tested, costs_tested, c=0.5, beta=0.7):
+    """Armijo line-search report of one iteration (:254-296).
+
+    The 200-point curve J(gamma) along the descent direction (:256-264; 200 closed-loop rollouts in the
+    reference) is one gym_gamma_sweep launch; the figure is the reference's (actual cost, first-order model
+    J + gamma dJ, Armijo line J + c gamma dJ, the tested and the accepted step sizes), drawn when matplotlib
+    is importable.  Returns the curve data {steps, costs, linear_approx, armijo_line} as well."""
+    max_step = max(1.25, max(stepsizes_tested) * 1.3 if stepsizes_tested else 1.25)
+    steps = np.linspace(0, max_step, 200)
+    x_traj = np.asarray(x_traj, dtype=float)
+    Nn = x_traj.shape[0]
+    costs = _eng().gamma_sweep(x_traj[None], np.asarray(u_traj, dtype=float)[None][:, :Nn - 1],
+                               np.asarray(K, dtype=float)[None], np.asarray(sigma, dtype=float)[None], steps,
+                               np.asarray(x_ref, dtype=float)[:Nn], np.asarray(u_ref, dtype=float)[:Nn - 1])
+    costs = costs[0].cpu().numpy()
+    curve = {"steps": steps, "costs": costs, "linear_approx": cost_current + delta_J * steps,
+             "armijo_line": cost_current + c * delta_J * steps}
+    _draw_armijo(iteration, curve, cost_current, delta_J, gamma_accepted, stepsizes_tested, costs_tested, c, beta,
+                 max_step)
+    return curve
+
+
+def _draw_armijo(iteration, curve, cost_current, delta_J, gamma_accepted, stepsizes_tested, costs_tested, c, beta,
+                 max_step):
+    try:
+        import matplotlib
+        import matplotlib.pyplot as plt
+    except ImportError:          # the report figure is optional; the curve is the computed result
+        return
+    steps = curve["steps"]
+    plt.figure(f'Armijo Line Search - Iteration {iteration}', figsize=(12, 7))
+    plt.clf()
+    plt.plot(steps, curve["costs"], color='blue', linewidth=2.5,
+             label=r'$J(x_k + \gamma \cdot \delta x, u_k + \gamma \cdot \delta u)$', alpha=0.8)
+    plt.plot(steps, curve["linear_approx"], color='red', linewidth=2.5, linestyle='--',
+             label=r'$J_k + \gamma \cdot \nabla J^T \delta$', alpha=0.8)
+    plt.plot(steps, curve["armijo_line"], color='green', linestyle='--', linewidth=2.5,
+             label=rf'$J_k + c \cdot \gamma \cdot \nabla J^T \delta$ (c={c})', alpha=0.8)
+    if stepsizes_tested and costs_tested:
+        plt.scatter(stepsizes_tested, costs_tested, marker='*', s=150, color='orange', edgecolor='black',
+                    linewidth=1.5, zorder=5, label=rf'Tested stepsizes ($\beta$={beta})')
+        plt.scatter(gamma_accepted, costs_tested[-1], marker='o', s=200, color='red', edgecolor='black',
+                    linewidth=2.5, zorder=6, label=rf'Accepted: $\gamma$={gamma_accepted:.4f}')
+    plt.xlabel(r'Step Size $\gamma$', fontsize=14)
+    plt.ylabel('Cost Value J', fontsize=14)
+    plt.title(f'Armijo Line Search - Iteration {iteration}\n' +
+              f'Current Cost = {cost_current:.4f}, Expected Reduction = {delta_J:.2e}', fontsize=15)
+    plt.grid(True, alpha=0.3)
+    plt.legend(fontsize=12, loc='best')
+    plt.xlim(0, max_step)
+    plt.tight_layout()
+    if matplotlib.get_backend().lower() not in ("agg", "pdf", "ps", "svg", "cairo", "template"):
+        plt.show()
 
 
 # ------------------------------------------------------------------------------ the solver
@@ -202,7 +263,7 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
     Tn = x_ref.shape[0] - 1
 
     def lane_x(buf):
-        return eng.unpack(solver.x[buf], 1)[0].cpu().numpy()
+        return eng.unpack(solver.states(buf), 1)[0].cpu().numpy()
 
     def lane_sigma():
         return solver.sigma()[0].cpu().numpy()
@@ -212,8 +273,14 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
         f"Simulated trajectory length mismatch: {x_traj.shape[0]} vs {x_ref.shape[0]}"
     cost_k = float(solver.cost[0].item())
     history = {"cost": [cost_k], "sigma_norm": [], "x_trajs": [x_traj.copy()], "sigmas": []}
+    trial_gammas = armijo_steps(gamma_0, beta, MAX_LINE_SEARCH_ITERS)
     for k in range(max_iters):
         prev_cost = cost_k
+        plot = (k < plot_armijo_iters and (k % 2 == 0 or k < 3)) or k == 1000    # :372-381
+        if plot:   # the trials' costs, bit for bit, and the pre-update iterate for the report
+            trial_costs = solver.gamma_sweep(trial_gammas)[0].cpu().numpy()
+            x_prev, u_prev = history["x_trajs"][-1], solver.controls(k & 1)[0].cpu().numpy()
+            rolls = int(solver.n_roll[0].item())
         solver.iteration()
         status = int(solver.status[0].item())
         sig = lane_sigma()
@@ -223,6 +290,13 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
             if verbose:
                 print(f"Iteration {k}: Line search failed to find sufficient decrease.")
             break
+        if plot:
+            n_tested = int(solver.n_roll[0].item()) - rolls
+            Kk = solver.gains()[0].cpu().numpy()
+            plot_armijo_line_search(k, x_prev, u_prev, [Kk[t] for t in range(Tn)], [sig[t] for t in range(Tn)],
+                                    prev_cost, x_ref, u_ref, float(solver.dJ[0].item()),
+                                    float(solver.gamma[0].item()), list(trial_gammas[:n_tested]),
+                                    list(trial_costs[:n_tested]), c, beta)
         cost_k = float(solver.cost[0].item())
         history["cost"].append(cost_k)
         history["x_trajs"].append(lane_x(solver.k & 1))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 2
+#define GYM_ABI_VERSION 3
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -46,6 +46,15 @@ extern "C" {
                              * at 0 and sigma0 = -(u0 - ur0) = -0, dynamics.py:205 ignores it), so the
                              * solver neither reads nor writes its planes; both u buffers are zeroed by
                              * gym_newton_init. Results are bit-identical to the general path.          */
+#define GYM_FLAG_X_CKPT 2   /* state checkpointing: the Armijo trials store x only at the checkpoint knots
+                             * t % GYM_CKPT_INTERVAL == 0 and t == N-1; the backward sweep re-integrates the
+                             * knots between two checkpoints (RK4 from the checkpoint with the stored controls,
+                             * the trial's own arithmetic, so bit-identical) instead of reading them: 48 B per
+                             * stage less HBM traffic, for 0.75 extra RK4 steps per sweep stage (opt-in: on
+                             * MI355X the solver kernels are VALU- as much as HBM-bound and it measured 13%
+                             * slower).  The other knots of x[] are stale until gym_newton_fill_states
+                             * rebuilds them (gym_newton_finalize does so itself).                          */
+#define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 
 /* Lane status codes (per-lane outcome of newton_Algorithm, trajectory_generation.py:329-396). */
@@ -201,11 +210,31 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
                      int32_t do_backward, void* stream);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
  * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
- * (sigma0 recomputed from that iteration's u0).  Any output may be NULL. */
-int gym_newton_finalize(const gym_weights* w, const gym_batch* bt, int32_t k_done, double* x_out, double* u_out,
-                        double* K_out, double* sigma_out, void* stream);
+ * (sigma0 recomputed from that iteration's u0).  Any output may be NULL.  With GYM_FLAG_X_CKPT the result
+ * buffers' states are first rebuilt from their checkpoints (gym_newton_fill_states, buf = -1). */
+int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batch* bt, int32_t k_done, double* x_out,
+                        double* u_out, double* K_out, double* sigma_out, void* stream);
+/* GYM_FLAG_X_CKPT: rebuild every knot of the state buffer x[buf] (buf = 0 / 1; -1 = each lane's result buffer
+ * res_buf) from its checkpoints and the controls u[buf]: x_{t+1} = RK4(x_t, u_t) from each checkpoint, the
+ * trial's arithmetic bit for bit.  Lanes [0, B); a no-op without the flag. */
+int gym_newton_fill_states(const gym_model* m, const gym_batch* bt, int32_t buf, void* stream);
 /* sigma (B,T,2) of each lane's most recent backward sweep (sigma1 from cs, sigma0 recomputed). */
 int gym_newton_sigma(const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);
+
+/* ---------------- Armijo gamma sweeps (plot_armijo_line_search, trajectory_generation.py:254-296) ---------------- */
+/* J(gamma_g) = total_cost (:231-252) of forward_closed_loop_update(x, u, K, sigma, gamma_g) (:218-229) for G step
+ * sizes per lane -- the reference's 200-point line-search curve (:258-264) -- cost only, one thread per
+ * (lane, step).  x (N,2,Bp) pairs, u and sigma (T,2,Bp) planes, Kf (T,4,Bp) full gains, gammas (G); cost_out
+ * (G,Bp), NaN for padding lanes. */
+int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, const double* u, const double* Kf,
+                    const double* sigma, const double* gammas, int32_t G, const double* x_ref, const double* u_ref,
+                    double* cost_out, int64_t B, int64_t Bp, int32_t N, void* stream);
+/* The same curve for every lane of a batched solve at the iterate iteration k starts from (k = iterations done;
+ * either schedule): runs iteration k's backward sweep (K1, cs, dJ, smax -- exactly what iteration k computes, so
+ * the solve is unaffected) and then the Armijo trial's own rollout for each gamma_g: at the trial's step sizes
+ * gamma0 beta^i the costs equal the trial costs bit for bit.  cost_out (G,Bp); NaN for lanes not ACTIVE. */
+int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_batch* bt, int32_t k,
+                           const double* gammas, int32_t G, double* cost_out, void* stream);
 
 /* ---------------- LQR / receding-horizon MPC trackers (trajectory_tracking.py) ---------------- */
 /* Time-varying LQR gains over windows of a stage array.  Stages: A (S,4,4), B (S,4,2) [device], continuous

@@ -207,6 +207,17 @@ def closed_loop(x, u, K, sig, gamma, pset=1):
     return xn, un
 
 
+def gamma_sweep(x, u, K, sig, gammas, x_ref, u_ref, Q=Q_DEFAULT, R=R_DEFAULT, QT=QT_DEFAULT, pset=1):
+    """plot_armijo_line_search's curve (trajectory_generation.py:256-264): for one trajectory x (N,4),
+    u (T,2), K (T,2,4), sigma (T,2), J(gamma) = total_cost(forward_closed_loop_update(..., gamma)) per
+    step size -> (G,).  The G rollouts run as G lanes of closed_loop."""
+    g = np.asarray(gammas, float).reshape(-1)
+    G = g.shape[0]
+    rep = lambda a: np.repeat(np.asarray(a, float)[None], G, axis=0)   # noqa: E731
+    xn, un = closed_loop(rep(x), rep(u), rep(K), rep(sig), g, pset=pset)
+    return total_cost(xn, un, x_ref, u_ref, Q, R, QT)
+
+
 # ---- the Newton / Armijo driver -----------------------------------------------------------------
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS = 0, 1, 2, 3
 

@@ -1,4 +1,5 @@
 import os
+os.environ.setdefault("MPLBACKEND", "Agg")   # the Armijo report figures of newton_Algorithm draw off-screen
 import sys
 
 import numpy as np

@@ -1,0 +1,129 @@
+"""Armijo line-search sweeps (plot_armijo_line_search, trajectory_generation.py:254-296) on the HIP path.
+
+Golden: tests/golden/armijo_sweep.npz, recorded from the reference's own plot_armijo_line_search during
+main.task_2's first 7 iterations (tests/golden/make_golden_armijo.py).  Tolerances: the curve values are
+costs of closed-loop rollouts computed with reordered arithmetic (closed-form dynamics), 1e-10 relative.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+def test_gamma_sweep_reproduces_reference_curve(golden):
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    g = golden("armijo_sweep")
+    eng = AcrobotEngine()
+    J = eng.gamma_sweep(g["k0_x"][None], g["k0_u"][None], g["k0_K"][None], g["k0_sigma"][None], g["k0_steps"],
+                        g["x_ref"], g["u_ref"]).cpu().numpy()
+    assert J.shape == (1, 200)
+    np.testing.assert_allclose(J[0], g["k0_costs"], rtol=TOL)
+    # several lanes at once: each lane's curve is independent of its neighbours
+    B = 70
+    rng = np.random.default_rng(5)
+    xs = np.repeat(g["k0_x"][None], B, 0)
+    xs[:, 0, :2] += rng.uniform(-0.05, 0.05, (B, 2))
+    us, Ks, ss = (np.repeat(g[k][None], B, 0) for k in ("k0_u", "k0_K", "k0_sigma"))
+    steps = g["k0_steps"][::7]
+    Jb = eng.gamma_sweep(xs, us, Ks, ss, steps, g["x_ref"], g["u_ref"]).cpu().numpy()
+    J1 = np.stack([eng.gamma_sweep(xs[b:b + 1], us[b:b + 1], Ks[b:b + 1], ss[b:b + 1], steps, g["x_ref"],
+                                   g["u_ref"]).cpu().numpy()[0] for b in (0, 33, 69)])
+    np.testing.assert_array_equal(Jb[[0, 33, 69]], J1)
+    from oracle import acrobot_np as onp
+    for b in (0, 33, 69):
+        np.testing.assert_allclose(Jb[b], onp.gamma_sweep(xs[b], us[b], Ks[b], ss[b], steps, g["x_ref"],
+                                                          g["u_ref"]), rtol=TOL)
+
+
+def test_newton_algorithm_armijo_reports_match_reference(golden, monkeypatch):
+    """newton_Algorithm(plot_armijo_iters=7) reports iterations 0, 1, 2, 4, 6 (:372-381) with the reference's
+    curves, tested step sizes and costs, and accepted step."""
+    from gymnast_optimalcontrol_amd import trajectory_generation as tg
+    g = golden("armijo_sweep")
+    seen = []
+    orig = tg.plot_armijo_line_search
+
+    def rec(iteration, *a, **k):
+        curve = orig(iteration, *a, **k)
+        seen.append((iteration, a, curve))
+        return curve
+
+    monkeypatch.setattr(tg, "plot_armijo_line_search", rec)
+    tg.newton_Algorithm(np.zeros(4), g["x_ref"], g["u_ref"], max_iters=7, tol=1e-4, gamma_0=0.1, plot_armijo_iters=7,
+                        verbose=False)
+    assert [s[0] for s in seen] == list(g["iters"])
+    for k, a, curve in seen:
+        p = f"k{k}_"
+        cost_current, delta_J, gamma_acc, tested, costs_tested = a[4], a[7], a[8], a[9], a[10]
+        np.testing.assert_array_equal(curve["steps"], g[p + "steps"])
+        np.testing.assert_allclose(curve["costs"], g[p + "costs"], rtol=TOL)
+        np.testing.assert_allclose(curve["linear_approx"], g[p + "lin"], rtol=TOL)
+        np.testing.assert_allclose(curve["armijo_line"], g[p + "arm"], rtol=TOL)
+        np.testing.assert_allclose(cost_current, g[p + "J"], rtol=TOL)
+        np.testing.assert_allclose(delta_J, g[p + "dJ"], rtol=1e-8)
+        assert gamma_acc == g[p + "gamma"]
+        np.testing.assert_array_equal(np.asarray(tested), g[p + "tested"])
+        np.testing.assert_allclose(costs_tested, g[p + "costs_tested"], rtol=TOL)
+    if seen[0][0] == 0:
+        a = seen[0][1]
+        np.testing.assert_allclose(np.asarray(a[2]), g["k0_K"], rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_solver_gamma_sweep_equals_trial_costs_and_leaves_solve_unchanged(task2_refs, pipeline):
+    """BatchedNewtonSolver.gamma_sweep at the trial step sizes gamma_0 beta^i gives the Armijo trials' costs
+    bit for bit (accepted step: the lane's new J; rejected ones fail the strict test), for every lane; and a
+    solve with sweeps between its iterations is bitwise the solve without them."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from gymnast_optimalcontrol_amd import _lib
+    xr, ur, _ = task2_refs
+    B = 300
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(8).uniform(-1.5, 1.5, (B, 2))
+    eng = AcrobotEngine()
+    # gamma_0 = 1 (the reference's default, :298): full steps backtrack from the first iterations and many lanes
+    # exhaust the 20 trials within 40 iterations (C oracle: every lane retries, 165 fail)
+    kw = dict(tol=1e-4, gamma_0=1.0, pipeline=pipeline)
+    s = BatchedNewtonSolver(eng, xr, ur, B, **kw)
+    s.max_iters = 40
+    s.init(x0)
+    from gymnast_optimalcontrol_amd.trajectory_generation import armijo_steps
+    gam = armijo_steps(1.0, 0.7, 20)
+    n_checked = n_retry = n_failed = 0
+    for _ in range(40):
+        J_prev = s.cost[:B].cpu().numpy().copy()
+        st_prev = s.status[:B].cpu().numpy().copy()
+        roll_prev = s.n_roll[:B].cpu().numpy().copy()
+        Jg = s.gamma_sweep(gam).cpu().numpy()
+        dJ = s.dJ[:B].cpu().numpy()
+        s.iteration()
+        st = s.status[:B].cpu().numpy(); J = s.cost[:B].cpu().numpy()
+        ntr = s.n_roll[:B].cpu().numpy() - roll_prev
+        act = st_prev == _lib.ACTIVE
+        assert np.isnan(Jg[~act]).all()
+        for b in np.nonzero(act & (st != _lib.LS_FAILED))[0]:
+            j = ntr[b] - 1
+            assert J[b] == Jg[b, j]
+            assert all(not (Jg[b, i] < J_prev[b] + 0.5 * gam[i] * dJ[b]) for i in range(j))
+            n_checked += 1
+            n_retry += j > 0
+        for b in np.nonzero(act & (st == _lib.LS_FAILED))[0]:   # every trial rejected (:361), no update
+            assert all(not (Jg[b, i] < J_prev[b] + 0.5 * gam[i] * dJ[b]) for i in range(20))
+            assert J[b] == J_prev[b]
+            n_failed += 1
+    assert n_checked > 1000 and n_retry > 100 and n_failed > 10
+    r_sweep = s
+    r_plain = BatchedNewtonSolver(eng, xr, ur, B, **kw)
+    r_plain.max_iters = 40
+    r_plain.init(x0)
+    for _ in range(40):
+        r_plain.iteration()
+    for name in ("cost", "status", "n_iter", "n_roll", "gamma"):
+        assert np.array_equal(getattr(r_sweep, name).cpu().numpy(), getattr(r_plain, name).cpu().numpy(),
+                              equal_nan=True), name
+    xa, ua, Ka, sa = r_sweep.finalize()
+    xb, ub, Kb, sb = r_plain.finalize()
+    for a, b in ((xa, xb), (ua, ub), (Ka, Kb), (sa, sb)):
+        assert np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True)

@@ -343,3 +343,38 @@ def test_u0_zero_stream_skipping_is_bitwise_identical(task2_refs, pipeline):
     assert not BatchedNewtonSolver(eng, xr, ur1, 4).u0_zero
     with pytest.raises(ValueError):
         BatchedNewtonSolver(eng, xr, ur1, 4, u0_zero=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline,u0z,N", [(False, True, 501), (True, True, 501), (False, False, 501),
+                                            (True, False, 203), (False, True, 6)])
+def test_state_checkpointing_is_bitwise_identical(task2_refs, pipeline, u0z, N):
+    """GYM_FLAG_X_CKPT (trials store every 4th knot, the sweep re-integrates the rest) gives bitwise the
+    full-store path's results -- trajectories, gains, sigma, costs, decisions, statistics -- incl. ragged
+    horizons (T % 4 != 0, T < 4) and backtracking / LS-failure / NaN lanes; states() rebuilds a buffer
+    mid-solve to the full-store buffer's bits."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    xr, ur = xr[:N], ur[:N - 1]
+    B = 600
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(44).uniform(-1.5, 1.5, (B, 2))
+    x0[5] = np.nan
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, pipeline=pipeline, u0_zero=None if u0z else False)
+    sc = BatchedNewtonSolver(eng, xr, ur, B, checkpoint=True, **kw)
+    sf = BatchedNewtonSolver(eng, xr, ur, B, checkpoint=False, **kw)
+    # mid-solve: 7 iterations, then the rebuilt current buffer equals the full-store one
+    for s in (sc, sf):
+        s.max_iters = 5000
+        s.init(x0)
+        for _ in range(7):
+            s.iteration()
+    buf = (7 & 1)
+    assert np.array_equal(sc.states(buf).cpu().numpy()[..., :B, :], sf.states(buf).cpu().numpy()[..., :B, :],
+                          equal_nan=True)
+    rc, rf = sc.solve(x0, 5000, keep_stats=True), sf.solve(x0, 5000, keep_stats=True)
+    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma"):
+        a, b = getattr(rc, name).cpu().numpy(), getattr(rf, name).cpu().numpy()
+        assert np.array_equal(a, b, equal_nan=True), name
+    assert np.array_equal(np.asarray(rc.stats_log), np.asarray(rf.stats_log), equal_nan=True)

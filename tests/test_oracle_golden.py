@@ -130,3 +130,16 @@ def test_c_oracle_task1_matches_reference(golden):
     assert rel_l2(r["x"][0], g["x"]) < 1e-8
     assert rel_l2(r["u"][0], g["u"]) < 1e-8
     assert np.abs(r["u"][0, :, 0]).max() > 0.1          # the tau1 channel is live in task 1
+
+
+def test_numpy_oracle_armijo_curve_matches_reference(golden):
+    """plot_armijo_line_search's 200-point curve (trajectory_generation.py:256-264), iteration 0 of task 2."""
+    g = golden("armijo_sweep")
+    c = onp.gamma_sweep(g["k0_x"], g["k0_u"], g["k0_K"], g["k0_sigma"], g["k0_steps"], g["x_ref"], g["u_ref"])
+    np.testing.assert_allclose(c, g["k0_costs"], rtol=1e-12)
+    np.testing.assert_array_equal(g["k0_steps"], np.linspace(0, 1.25, 200))
+    np.testing.assert_allclose(g["k0_lin"], g["k0_J"] + g["k0_dJ"] * g["k0_steps"], rtol=1e-15)
+    # the accepted trial's cost is the curve's value at that step size
+    c1 = onp.gamma_sweep(g["k0_x"], g["k0_u"], g["k0_K"], g["k0_sigma"], g["k0_tested"], g["x_ref"],
+                         g["u_ref"])
+    np.testing.assert_allclose(c1, g["k0_costs_tested"], rtol=1e-13)

@@ -2,7 +2,8 @@
 """Interleaved A/B timing of library variants in ONE process on one device (measurement tool).
 
     python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so:serial lib_b.so:pipe:nou0z ...
-(":serial" / ":pipe" select the schedule, ":nou0z" disables the tau1 = 0 stream skipping; default:
+(":serial" / ":pipe" select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":nock" the state
+checkpointing; default:
 the solver's choice)
 Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
 kernel library is swapped), so buffer placement -- worth +-4% on its own -- is held fixed; prints
@@ -36,7 +37,8 @@ def main():
     def split(spec):
         path, *opts = spec.split(":")
         sched = {"serial": False, "pipe": True}
-        return os.path.abspath(path), next((sched[o] for o in opts if o in sched), None), "nou0z" not in opts
+        return (os.path.abspath(path), next((sched[o] for o in opts if o in sched), None), "nou0z" not in opts,
+                "nock" not in opts)
     eng = AcrobotEngine(lib_path=split(a.libs[0])[0])
     s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1).enable_timing()
     default_pipe = s.pipeline
@@ -47,10 +49,11 @@ def main():
     for r in range(a.rounds + 1):
         for p in a.libs:
             eng.lib = libs[p]
-            _, sched, u0z = split(p)
+            _, sched, u0z, ck = split(p)
             s.pipeline = default_pipe if sched is None else sched
             s.u0_zero = default_u0z and u0z
-            s.batch.flags = _lib.FLAG_U0_ZERO if s.u0_zero else 0
+            s.checkpoint = ck
+            s.batch.flags = (_lib.FLAG_U0_ZERO if s.u0_zero else 0) | (_lib.FLAG_X_CKPT if ck else 0)
             s.reset_timing()
             out = s.solve(xd, a.max_iters)
             kt = s.kernel_times()
