@@ -152,7 +152,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=262144, help="lanes per GPU (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="lanes per GPU (weak scaling); default 262144 (newton, cfg 3) or 8192 (mpc, cfg 5)")
     ap.add_argument("--max-iters", type=int, default=5000)
     ap.add_argument("--cpu-lanes", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
@@ -161,11 +162,13 @@ def main():
                     help="outer iterations between host reads of the (all-reduced) statistics; iterations "
                          "enqueued after every lane has finished are no-ops")
     ap.add_argument("--workload", choices=("newton", "mpc"), default="newton",
-                    help="newton: the north-star metric (cfg 3); mpc: BASELINE cfg 5 (use --batch 8192)")
+                    help="newton: the north-star metric (cfg 3); mpc: BASELINE cfg 5")
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined"), default="auto",
                     help="solver schedule (auto: the solver's choice for the batch size)")
     a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 8192 if a.workload == "mpc" else 262144
     if a.workload == "mpc":
         return run_mpc(a)
 

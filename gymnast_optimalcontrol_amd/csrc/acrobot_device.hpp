@@ -35,18 +35,36 @@ struct Dyn {
 // a non-finite trajectory.  Keeping ocml's full-range path out of the kernels saves ~25 VGPRs.
 // ------------------------------------------------------------------------------------------
 // fdlibm minimax kernels: sin(r), cos(r) for |r| <= pi/4.
-__device__ __forceinline__ double ksin(double r, double z) {
-    return fma(r * z, fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+// The innermost Horner step fma(z, C6, C5) has two constant operands; a VALU instruction reads at most
+// one SGPR/literal, so the compiler re-materialises one of them with a v_mov_b64 at every use (16 per
+// RK4 step).  PolyRegs carries those four coefficients; a stage loop takes a VGPR-resident copy
+// (poly_vgprs) once, outside the loop.  Same constants, same operations: the same bits.
+struct PolyRegs {
+    double s6, s5, c6, c5;
+};
+__device__ __forceinline__ PolyRegs poly_lits() {
+    return PolyRegs{1.58969099521155010221e-10, -2.50507602534068634195e-08, -1.13596475577881948265e-11,
+                    2.08757232129817482790e-09};
+}
+__device__ __forceinline__ void in_vgpr(double& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ PolyRegs poly_vgprs() {
+    PolyRegs k = poly_lits();
+    in_vgpr(k.s6); in_vgpr(k.s5); in_vgpr(k.c6); in_vgpr(k.c5);
+    return k;
+}
+
+__device__ __forceinline__ double ksin(double r, double z, const PolyRegs& k) {
+    return fma(r * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.s6, k.s5),
         2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
         -1.66666666666666324348e-01), r);
 }
-__device__ __forceinline__ double kcos(double z) {
-    return fma(z * z, fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+__device__ __forceinline__ double kcos(double z, const PolyRegs& k) {
+    return fma(z * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.c6, k.c5),
         -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
         4.16666666666666019037e-02), fma(-0.5, z, 1.0));
 }
 
-__device__ __forceinline__ void fast_sincos(double x, double* s, double* c) {
+__device__ __forceinline__ void fast_sincos(double x, double* s, double* c, const PolyRegs& k = poly_lits()) {
     constexpr double kTwoOverPi = 6.36619772367581382433e-01;
     constexpr double kPio2Hi = 1.57079632679489655800e+00;   // 0x3FF921FB54442D18
     constexpr double kPio2Lo = 6.12323399573676603587e-17;   // 0x3C91A62633145C07
@@ -54,8 +72,8 @@ __device__ __forceinline__ void fast_sincos(double x, double* s, double* c) {
     const double qn = (fabs(kq) < 1048576.0) ? kq : __builtin_nan("");   // outside the domain: NaN
     const double r = fma(-qn, kPio2Lo, fma(-qn, kPio2Hi, x));
     const double z = r * r;
-    const double sr = ksin(r, z);
-    const double cr = kcos(z);
+    const double sr = ksin(r, z, k);
+    const double cr = kcos(z, k);
     const int q = (int)qn;                 // v_cvt_i32_f64 maps NaN to 0
     const double ss = (q & 1) ? cr : sr;   // quadrant rotation
     const double cc = (q & 1) ? sr : cr;
@@ -109,43 +127,44 @@ __device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, dou
 // rotation, ~20 VALU instead of ~40 for a reduction from scratch.  d = (h/2) w or h w is small; a lane
 // with |d| > pi/4 (|w| > 39 rad/s) reduces both arguments from scratch instead.  The choice is per lane,
 // so a lane's arithmetic never depends on which other lanes share its wavefront.
-__device__ __forceinline__ void rotate(double s, double c, double d, double& so, double& co) {
+__device__ __forceinline__ void rotate(double s, double c, double d, double& so, double& co, const PolyRegs& k) {
     const double z = d * d;
-    const double sd = ksin(d, z), cd = kcos(z);
+    const double sd = ksin(d, z, k), cd = kcos(z, k);
     so = fma(s, cd, c * sd);
     co = fma(c, cd, -(s * sd));
 }
 
 __device__ __forceinline__ void substep_sincos(double th1, double th2, double d1, double d2, double s1, double c1,
                                                double s2, double c2, double& t1, double& u1, double& t2,
-                                               double& u2) {
+                                               double& u2, const PolyRegs& k) {
     constexpr double kPio4 = 0.78539816339744830962;
     if (__builtin_expect(fabs(d1) <= kPio4 && fabs(d2) <= kPio4, 1)) {
-        rotate(s1, c1, d1, t1, u1);
-        rotate(s2, c2, d2, t2, u2);
+        rotate(s1, c1, d1, t1, u1, k);
+        rotate(s2, c2, d2, t2, u2, k);
     } else {   // also taken by NaN lanes
-        fast_sincos(th1 + d1, &t1, &u1);
-        fast_sincos(th2 + d2, &t2, &u2);
+        fast_sincos(th1 + d1, &t1, &u1, k);
+        fast_sincos(th2 + d2, &t2, &u2, k);
     }
 }
 
 // Classic RK4 with the control held over the step (dynamics.py:177-195), in place.  Only the step's
 // base angles are reduced from scratch; the three sub-step states' angles x + d, d = (h/2) k1, (h/2) k2,
 // h k3, get their sin/cos by angle addition (substep_sincos).
-__device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2) {
+__device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2,
+                                    const PolyRegs& k = poly_lits()) {
     double a1, b1, a2, b2, a3, b3, a4, b4;
     double s1, c1, s2, c2, t1, u1, t2, u2;
-    fast_sincos(x0, &s1, &c1);
-    fast_sincos(x1, &s2, &c2);
+    fast_sincos(x0, &s1, &c1, k);
+    fast_sincos(x1, &s2, &c2, k);
     accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
     const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
-    substep_sincos(x0, x1, m.h2 * x2, m.h2 * x3, s1, c1, s2, c2, t1, u1, t2, u2);
+    substep_sincos(x0, x1, m.h2 * x2, m.h2 * x3, s1, c1, s2, c2, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
     const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
-    substep_sincos(x0, x1, m.h2 * y2, m.h2 * y3, s1, c1, s2, c2, t1, u1, t2, u2);
+    substep_sincos(x0, x1, m.h2 * y2, m.h2 * y3, s1, c1, s2, c2, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
     const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
-    substep_sincos(x0, x1, m.h * z2, m.h * z3, s1, c1, s2, c2, t1, u1, t2, u2);
+    substep_sincos(x0, x1, m.h * z2, m.h * z3, s1, c1, s2, c2, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
     const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
     const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;
@@ -160,10 +179,11 @@ struct Jac {
     double a2[4], a3[4], bc2, bc3;
 };
 
-__device__ __forceinline__ Jac jacobian(const Dyn& m, double th1, double th2, double w1, double w2, double tau2) {
+__device__ __forceinline__ Jac jacobian(const Dyn& m, double th1, double th2, double w1, double w2, double tau2,
+                                        const PolyRegs& k = poly_lits()) {
     double s1, c1, s2, c2;
-    fast_sincos(th1, &s1, &c1);
-    fast_sincos(th2, &s2, &c2);
+    fast_sincos(th1, &s1, &c1, k);
+    fast_sincos(th2, &s2, &c2, k);
     const double s12 = s1 * c2 + c1 * s2, c12 = c1 * c2 - s1 * s2;
     const double bs2 = m.b * s2, bc2 = m.b * c2;
     const double M11 = m.a2b + 2.0 * bc2, M12 = m.d + bc2;

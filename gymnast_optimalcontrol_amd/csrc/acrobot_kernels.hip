@@ -134,6 +134,7 @@ __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 // The stage index is wave-uniform: these are scalar compares and s_setprio, no VALU.
 __device__ __forceinline__ void prio_start() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ void prio_band(int done, int T) {
+    asm volatile("" : "+s"(T));   // thresholds recomputed per stage (3 SALU) rather than held: no spills
     if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
     else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
     else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
@@ -239,6 +240,7 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         q.c = bld2<CP>(rsrc(Cb + (int64_t)t * row), o2, 0);
         q.u0 = U0Z ? 0.0 : bld1<CP>(rsrc(Ub + (int64_t)t * row), o1, 0);
     };
+    const gym::PolyRegs pk = gym::poly_vgprs();   // loop-invariant coefficients held in VGPRs
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
     fetch(pre, 0);
     pin(pre.k0); pin(pre.k1); pin(pre.c); pin(pre.u0);
@@ -254,14 +256,20 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
         const double v1 = (c.x + kx) + gamma * c.y;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
+#ifndef GYM_NO_KARG
+        const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
+        J += xcost(ka.w.Q, n0, n1, n2, n3, xr + 4 * t);
+        J += f0 * (ka.w.R[0] * f0) + f1 * (ka.w.R[1] * f1);
+#else
         J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
         J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
+#endif
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
             if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
             bst1(rO, o1, plane, v1);
         }
-        gym::rk4(m, n0, n1, n2, n3, v1);
+        gym::rk4(m, n0, n1, n2, n3, v1, pk);
         if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
             bst2(rX, o2, 0, n0, n1);
@@ -296,9 +304,10 @@ struct Sweep {
     // stage t (x_t = (xa, xb), u_t = (ut0, ut1)): gain row 1 k[0..3], sigma (s0, s1); updates P, p, dJ, smax
     __device__ __forceinline__ void step(const Dyn& m, const KW& w, double2 xa, double2 xb, double ut0, double ut1,
                                          const double* xrt, const double* urt, double& k0, double& k1,
-                                         double& k2, double& k3, double& s0, double& s1) {
+                                         double& k2, double& k3, double& s0, double& s1,
+                                         const gym::PolyRegs& pk = gym::poly_lits()) {
         const double dt = m.h;
-        const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1);
+        const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1, pk);
         // A_d rows 2,3 (rows 0,1 = [1 0 dt 0], [0 1 0 dt]); B_d = dt * [0 0 bc2 bc3]^T in column 1
         const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
         const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
@@ -417,6 +426,7 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
     const char* Kb = reinterpret_cast<const char*>(K1);
     const char* Cb = reinterpret_cast<const char*>(cs);
     Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    const gym::PolyRegs pk = gym::poly_vgprs();
     double2 pa, pb;
     double pu0 = 0.0, pu1;
     {
@@ -439,8 +449,12 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
             pu1 = bld1(rU, o1, plane);
         }
         double k0, k1, k2, k3, s0, s1;
+#ifndef GYM_NO_KARG
         const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
-        S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
+#else
+        S.step(m, w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
+#endif
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         bst2(rK, o2, 0, k0, k1);
