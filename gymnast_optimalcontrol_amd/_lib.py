@@ -100,7 +100,7 @@ _SIGS = {
     "gym_tv_lqr_gains": [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _D, _P, _P],
     "gym_dare_fixed_point": [_P, _P, _P, _P, _I32, _D, _P, _P, _P],
     "gym_lq_forward": [_P, _P, _I32, _P, _P, _I32, _D, _P, _P, _I32, _P, _P, _P],
-    "gym_track_rollout": [_MP, _P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _P],
+    "gym_track_rollout": [_MP, _P, _P, _P, _P, _I64, _I32, _P, _P, _P],
     "gym_timing_create": [C.POINTER(GymTiming)],
     "gym_timing_destroy": [C.POINTER(GymTiming)],
     "gym_timing_collect": [C.POINTER(GymTiming)],

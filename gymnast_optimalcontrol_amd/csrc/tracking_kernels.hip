@@ -84,14 +84,15 @@ __device__ __forceinline__ void load_stage(const double* A, const double* Bm, in
 // all_gains: K_out (L-1, 2, 4) of window 0;  else K_out (nwin, 2, 4) = the first gain of every window.
 __global__ __launch_bounds__(64) void k_tv_lqr_gains(const double* __restrict__ A, const double* __restrict__ Bm,
                                                      int S, const double* __restrict__ Ap,
-                                                     const double* __restrict__ Bp, M44 Q, M22 R, M44 QT, int L,
+                                                     const double* __restrict__ Bp, M44 Q, M22 R,
+                                                     const double* __restrict__ QT, int L,
                                                      int nwin, int all_gains, int disc, double dt,
                                                      double* __restrict__ K_out) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nwin) return;
     double P[16], K[8], Ad[16], Bd[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) P[k] = QT.v[k];
+    for (int k = 0; k < 16; ++k) P[k] = QT[k];
     for (int s = L - 2; s >= 0; --s) {
         load_stage(A, Bm, w + s, S, Ap, Bp, disc, dt, Ad, Bd);
         lqr_step(Ad, Bd, P, Q, R, K);
@@ -106,29 +107,61 @@ __global__ __launch_bounds__(64) void k_tv_lqr_gains(const double* __restrict__ 
     }
 }
 
-// compute_P_inf (:144-165): P <- Riccati map of (A, B, Q, R) from P = Q until max|dP| < tol (single thread)
-__global__ void k_dare_fixed_point(const double* __restrict__ A, const double* __restrict__ Bm, M44 Q, M22 R,
-                                   int max_iter, double tol, double* __restrict__ P_out, int32_t* __restrict__ iters) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    double a[16], b[8], P[16], K[8];
+// compute_P_inf (:144-165): P <- Riccati map of (A, B, Q, R) from P = Q until max|dP| < tol.  One wavefront;
+// lane 4i+j (< 16) owns P[i][j] and evaluates that entry of every product of the map (the same sums, in
+// the same order, as one lane would), exchanging rows/columns through LDS: each iteration is a few
+// dependent steps instead of ~400 dependent flops of a single lane.  max|dP| is a wave reduction.
+__global__ __launch_bounds__(64) void k_dare_fixed_point(const double* __restrict__ A, const double* __restrict__ Bm,
+                                                         M44 Q, M22 R, int max_iter, double tol,
+                                                         double* __restrict__ P_out, int32_t* __restrict__ iters) {
+    __shared__ double sP[16], sPA[16], sPB[8];
+    const int ln = threadIdx.x, i = (ln >> 2) & 3, j = ln & 3;
+    const bool own = ln < 16;
+    double a[16], b[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { a[k] = A[k]; P[k] = Q.v[k]; }
+    for (int k = 0; k < 16; ++k) a[k] = A[k];
 #pragma unroll
     for (int k = 0; k < 8; ++k) b[k] = Bm[k];
+    double P = Q.v[4 * i + j];
     int it = max_iter;
-    for (int i = 0; i < max_iter; ++i) {
-        double prev[16];
+    for (int n = 0; n < max_iter; ++n) {
+        if (own) sP[ln] = P;
+        __syncthreads();
+        const double* Pi = sP + 4 * i;   // row i of P
+        const double PA = ((Pi[0] * a[j] + Pi[1] * a[4 + j]) + Pi[2] * a[8 + j]) + Pi[3] * a[12 + j];
+        const double PB0 = ((Pi[0] * b[0] + Pi[1] * b[2]) + Pi[2] * b[4]) + Pi[3] * b[6];
+        const double PB1 = ((Pi[0] * b[1] + Pi[1] * b[3]) + Pi[2] * b[5]) + Pi[3] * b[7];
+        if (own) {
+            sPA[ln] = PA;
+            if (j == 0) { sPB[2 * i] = PB0; sPB[2 * i + 1] = PB1; }
+        }
+        __syncthreads();
+        double a1[4];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) prev[k] = P[k];
-        lqr_step(a, b, P, Q, R, K);
-        double d = 0.0;
+        for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d = fmax(d, fabs(P[k] - prev[k]));
-        if (d < tol) { it = i + 1; break; }
+            for (int c = 0; c < 2; ++c)
+                a1[2 * r + c] = R.v[2 * r + c] + (((b[r] * sPB[c] + b[2 + r] * sPB[2 + c]) + b[4 + r] * sPB[4 + c]) +
+                                                  b[6 + r] * sPB[6 + c]);
+        const double a20 = ((b[0] * sPA[j] + b[2] * sPA[4 + j]) + b[4] * sPA[8 + j]) + b[6] * sPA[12 + j];
+        const double a21 = ((b[1] * sPA[j] + b[3] * sPA[4 + j]) + b[5] * sPA[8 + j]) + b[7] * sPA[12 + j];
+        const double idet = 1.0 / (a1[0] * a1[3] - a1[1] * a1[2]);
+        const double i00 = a1[3] * idet, i01 = -a1[1] * idet, i10 = -a1[2] * idet, i11 = a1[0] * idet;
+        const double K0 = -(i00 * a20 + i01 * a21), K1 = -(i10 * a20 + i11 * a21);
+        const double apa = ((a[i] * sPA[j] + a[4 + i] * sPA[4 + j]) + a[8 + i] * sPA[8 + j]) + a[12 + i] * sPA[12 + j];
+        const double apb0 = ((a[i] * sPB[0] + a[4 + i] * sPB[2]) + a[8 + i] * sPB[4]) + a[12 + i] * sPB[6];
+        const double apb1 = ((a[i] * sPB[1] + a[4 + i] * sPB[3]) + a[8 + i] * sPB[5]) + a[12 + i] * sPB[7];
+        const double nP = (Q.v[4 * i + j] + apa) + (apb0 * K0 + apb1 * K1);
+        double d = own ? fabs(nP - P) : 0.0;
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) d = fmax(d, __shfl_xor(d, off, 64));
+        d = __shfl(d, 0, 64);
+        P = nP;
+        __syncthreads();   // every lane has read sP / sPA / sPB before the next iteration rewrites them
+        if (d < tol) { it = n + 1; break; }
     }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) P_out[k] = P[k];
-    *iters = it;
+    if (own) P_out[ln] = P;
+    if (ln == 0) *iters = it;
 }
 
 // LQ forward pass of one window (solver_mpc's X_opt, U_opt): x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s
@@ -157,28 +190,44 @@ __global__ void k_lq_forward(const double* __restrict__ A, const double* __restr
 
 // Batched closed-loop tracking simulation (simulate_tracking :206-216; MPC loop :43-60):
 //   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
-// x0 (B,4) lane-major; shared x_ff (N,4), u_ff (T,2), K (T,2,4); out x (N,2,Bp) pairs, u (T,2,Bp) planes.
+// x0 (B,4); shared x_ff (N,4), u_ff (T,2), K (T,2,4); outputs lane-major x (B,N,4), u (B,T,2).  Each lane is a
+// chain of T dependent RK4 steps (B/64 wavefronts: latency-bound), so the step's shared operands are loaded
+// one step ahead (wave-uniform, scalar) and the lane writes its own rows directly: consecutive steps fill
+// its 128-B lines in L2, no transpose pass afterwards.
 __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __restrict__ x0,
                                                       const double* __restrict__ x_ff, const double* __restrict__ u_ff,
-                                                      const double* __restrict__ K, int64_t B, int64_t Bp, int N,
-                                                      double2* __restrict__ xo, double* __restrict__ uo) {
+                                                      const double* __restrict__ K, int64_t B, int N,
+                                                      double* __restrict__ xo, double* __restrict__ uo) {
     const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= B) return;
     const int T = N - 1;
+    double2* xl = reinterpret_cast<double2*>(xo + 4 * (int64_t)N * l);
+    double2* ul = reinterpret_cast<double2*>(uo + 2 * (int64_t)T * l);
     double n0 = x0[4 * l], n1 = x0[4 * l + 1], n2 = x0[4 * l + 2], n3 = x0[4 * l + 3];
-    xo[l] = make_double2(n0, n1);
-    xo[Bp + l] = make_double2(n2, n3);
+    xl[0] = make_double2(n0, n1);
+    xl[1] = make_double2(n2, n3);
+    double k[8], r[4], f[2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) k[q] = K[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
+    f[0] = u_ff[0]; f[1] = u_ff[1];
     for (int t = 0; t < T; ++t) {
-        const double* k = K + 8 * t;
-        const double* xr = x_ff + 4 * t;
-        const double d0 = n0 - xr[0], d1 = n1 - xr[1], d2 = n2 - xr[2], d3 = n3 - xr[3];
-        const double v0 = u_ff[2 * t] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
-        const double v1 = u_ff[2 * t + 1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
-        uo[(2 * (int64_t)t) * Bp + l] = v0;
-        uo[(2 * (int64_t)t + 1) * Bp + l] = v1;
+        const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
+        const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
+        const double v1 = f[1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+        if (t + 1 < T) {   // next step's shared operands, in flight during this step's RK4
+            const double* kn = K + 8 * (t + 1);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) k[q] = kn[q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = x_ff[4 * (t + 1) + q];
+            f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
+        }
+        ul[t] = make_double2(v0, v1);
         gym::rk4(m, n0, n1, n2, n3, v1);
-        xo[(2 * (int64_t)(t + 1)) * Bp + l] = make_double2(n0, n1);
-        xo[(2 * (int64_t)(t + 1) + 1) * Bp + l] = make_double2(n2, n3);
+        xl[2 * (t + 1)] = make_double2(n0, n1);
+        xl[2 * (t + 1) + 1] = make_double2(n2, n3);
     }
 }
 
@@ -197,7 +246,7 @@ int gym_tv_lqr_gains(const double* A, const double* Bm, int32_t S, const double*
         return GYM_EINVAL;
     if ((nwin - 1) + (L - 2) >= S && (!A_pad || !B_pad)) return GYM_EINVAL;   // a window runs past the stages
     hipLaunchKernelGGL(k_tv_lqr_gains, dim3((nwin + 63) / 64), dim3(64), 0, (hipStream_t)s, A, Bm, S, A_pad, B_pad,
-                       m44(Q), m22(R), m44(QT), L, nwin, all_gains, discretize, dt, K_out);
+                       m44(Q), m22(R), QT, L, nwin, all_gains, discretize, dt, K_out);
     return launch_status();
 }
 
@@ -220,12 +269,11 @@ int gym_lq_forward(const double* A, const double* Bm, int32_t S, const double* A
 }
 
 int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
-                      int64_t B, int64_t Bp, int32_t N, double* x_out, double* u_out, void* s) {
-    if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || Bp < B || (Bp % 64) != 0 ||
-        Bp > GYM_MAX_BP || N < 2)
+                      int64_t B, int32_t N, double* x_out, double* u_out, void* s) {
+    if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || B > ((int64_t)1 << 31) || N < 2)
         return GYM_EINVAL;
     hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, Dyn(*m), x0, x_ff,
-                       u_ff, K, B, Bp, N, (double2*)x_out, u_out);
+                       u_ff, K, B, N, x_out, u_out);
     return launch_status();
 }
 

@@ -326,16 +326,17 @@ class AcrobotEngine:
         S = A.shape[0]
         Ap = None if A_pad is None else self.t(A_pad).reshape(4, 4)
         Bp_ = None if B_pad is None else self.t(B_pad).reshape(4, 2)
-        Qh, Rh, QTh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R"), self._host_mat(QT, 4, "Q_T")
+        Qh, Rh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R")
+        QTd = self.t(QT).reshape(4, 4)                 # device: e.g. dare_fixed_point's P, no host round trip
         out = torch.empty(((L - 1) if all_gains else nwin, 2, 4), dtype=F64, device=self.device)
         _lib.check(self.lib.gym_tv_lqr_gains(A.data_ptr(), Bm.data_ptr(), S, _lib.ptr(Ap), _lib.ptr(Bp_),
-                                             Qh.ctypes.data, Rh.ctypes.data, QTh.ctypes.data, int(L), int(nwin),
+                                             Qh.ctypes.data, Rh.ctypes.data, QTd.data_ptr(), int(L), int(nwin),
                                              int(bool(all_gains)), int(bool(discretize)), self.dt, out.data_ptr(),
                                              self.stream), "gym_tv_lqr_gains")
         return out
 
     def dare_fixed_point(self, A, Bm, Q, R, max_iter: int = 1000, tol: float = 1e-6):
-        """compute_P_inf on the device: returns (P (4,4) tensor, iterations)."""
+        """compute_P_inf on the device: returns (P (4,4), iterations (1,) int32), both device tensors (no sync)."""
         A = self.t(A).reshape(4, 4); Bm = self.t(Bm).reshape(4, 2)
         Qh, Rh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R")
         P = torch.empty((4, 4), dtype=F64, device=self.device)
@@ -343,7 +344,7 @@ class AcrobotEngine:
         _lib.check(self.lib.gym_dare_fixed_point(A.data_ptr(), Bm.data_ptr(), Qh.ctypes.data, Rh.ctypes.data,
                                                  int(max_iter), float(tol), P.data_ptr(), it.data_ptr(), self.stream),
                    "gym_dare_fixed_point")
-        return P, int(it.item())
+        return P, it
 
     def lq_forward(self, A, Bm, K, x0, L: int, A_pad=None, B_pad=None, discretize: bool = False):
         """One window's LQ forward pass: X (L,4), U (L-1,2)."""
@@ -366,10 +367,9 @@ class AcrobotEngine:
         if u_ff.shape[0] != N - 1 or K.shape[0] != N - 1:
             raise ValueError(f"feed-forward / gains must hold {N - 1} stages, got {u_ff.shape[0]} / {K.shape[0]}")
         B = x0.shape[0]
-        Bp = padded(B)
-        xs = torch.empty((N, 2, Bp, 2), dtype=F64, device=self.device)
-        us = torch.empty((N - 1, 2, Bp, 1), dtype=F64, device=self.device)
+        x = torch.empty((B, N, 4), dtype=F64, device=self.device)
+        u = torch.empty((B, N - 1, 2), dtype=F64, device=self.device)
         _lib.check(self.lib.gym_track_rollout(C.byref(self.model), x0.data_ptr(), x_ff.data_ptr(), u_ff.data_ptr(),
-                                              K.data_ptr(), B, Bp, N, xs.data_ptr(), us.data_ptr(), self.stream),
+                                              K.data_ptr(), B, N, x.data_ptr(), u.data_ptr(), self.stream),
                    "gym_track_rollout")
-        return self.unpack(xs, B), self.unpack(us, B)
+        return x, u

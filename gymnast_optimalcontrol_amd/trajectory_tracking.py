@@ -50,7 +50,7 @@ def compute_P_inf(A, B, Q, R):
     eng = _eng()
     P, it = eng.dare_fixed_point(A, B, Q, R, max_iter=1000, tol=1e-6)
     P = _np(P)
-    if it >= 1000 and not np.isfinite(P).all():
+    if int(it.item()) >= 1000 and not np.isfinite(P).all():
         print("P_inf did not converge!!!")
     return P
 
@@ -106,7 +106,7 @@ def mpc_gains(x_ref, u_ref, T_pred: int = T_PRED, Q=Q_MPC, R=R_MPC, n_steps: int
     Af_c, Bf_c = eng.jacobians(X_F.reshape(1, 4), U_F.reshape(1, 2))
     A_f, B_f = _discrete(eng, Af_c[0], Bf_c[0])
     QT, _ = eng.dare_fixed_point(A_f, B_f, Q, R)
-    K0 = eng.tv_lqr_gains(A_c, B_c, Q, R, _np(QT), L=int(T_pred), nwin=n_steps, all_gains=False,
+    K0 = eng.tv_lqr_gains(A_c, B_c, Q, R, QT, L=int(T_pred), nwin=n_steps, all_gains=False,
                           A_pad=Af_c[0], B_pad=Bf_c[0], discretize=True)
     return K0, QT
 

@@ -244,7 +244,7 @@ int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_b
  * over stages w+L-2 .. w from P = QT.  all_gains != 0 (nwin == 1): K_out (L-1,2,4) = every gain
  * (solve_LQR_tracking :170-203 with L = S+1);  else K_out (nwin,2,4) = each window's first gain, the exact
  * solution u0 = K x0 of solver_mpc's equality-constrained QP (:73-140, T_pred = L) at control step w
- * (solve_mpc_tracking :8-69).  Q, R, QT [host].                                                                  */
+ * (solve_mpc_tracking :8-69).  Q, R [host]; QT (4,4) [device] (e.g. gym_dare_fixed_point's P, no host round trip). */
 int gym_tv_lqr_gains(const double* A, const double* B, int32_t S, const double* A_pad, const double* B_pad,
                      const double Q[16], const double R[4], const double QT[16], int32_t L, int32_t nwin,
                      int32_t all_gains, int32_t discretize, double dt, double* K_out, void* stream);
@@ -259,9 +259,9 @@ int gym_lq_forward(const double* A, const double* B, int32_t S, const double* A_
                    void* stream);
 /* Batched closed-loop tracking (simulate_tracking :206-216; the MPC loop :43-60):
  *   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
- * x0 (B,4) lane-major; shared x_ff (N,4), u_ff (T,2), K (T,2,4); x_out (N,2,Bp) pairs, u_out (T,2,Bp) planes. */
+ * x0 (B,4); shared x_ff (N,4), u_ff (T,2), K (T,2,4); lane-major x_out (B,N,4), u_out (B,T,2). */
 int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
-                      int64_t B, int64_t Bp, int32_t N, double* x_out, double* u_out, void* stream);
+                      int64_t B, int32_t N, double* x_out, double* u_out, void* stream);
 
 /* [host] create / destroy the events of a gym_timing; collect = add the elapsed time of every pending
  * pair (call only after the stream that recorded them has been synchronised). */

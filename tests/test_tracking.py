@@ -133,4 +133,5 @@ def test_tracking_abi_rejects_bad_arguments():
     assert lib.gym_tv_lqr_gains(1, 1, 100, None, None, Q.ctypes.data, R.ctypes.data, Q.ctypes.data, 20, 2, 1, 0,
                                 0.02, 1, None) == 1
     m = _lib.GymModel()
-    assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 100, 100, 501, 1, 1, None) == 1   # Bp not a multiple of 64
+    assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 0, 501, 1, 1, None) == 1          # empty batch
+    assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 100, 1, 1, 1, None) == 1          # N < 2
