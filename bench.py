@@ -177,7 +177,7 @@ def main():
     rank, local_rank, world = gd.init_process_group()
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(gd.local_device_index(local_rank))
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
 

@@ -106,6 +106,13 @@ __device__ __forceinline__ void st_nt(double* p, double a) { __builtin_nontempor
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 constexpr int kNT = 2;  // gfx950 cache-policy bits: nt (streamed once)
+#ifndef GYM_SW_LD
+#define GYM_SW_LD 2
+#endif
+#ifndef GYM_SW_ST
+#define GYM_SW_ST 2
+#endif
+constexpr int SW_LD = GYM_SW_LD, SW_ST = GYM_SW_ST;   // the solver sweep's load / store policies
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
@@ -117,8 +124,9 @@ template <int CP = kNT>
 __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, CP));
 }
+template <int CP = kNT>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a, double b) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, kNT);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, CP);
 }
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, kNT);
@@ -132,12 +140,27 @@ __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 // / 2.49 ms of a 2.5 ms launch), so the launch ends with one wave per SIMD and few loads in flight.  With
 // the bands the lagging waves win arbitration, all finish together, and the launch is 6% shorter.
 // The stage index is wave-uniform: these are scalar compares and s_setprio, no VALU.
-__device__ __forceinline__ void prio_start() { __builtin_amdgcn_s_setprio(3); }
+// KIND: 0 = sweep, 1 = trial.  GYM_PRIO_MODE (experiments): 0 both 3..0 by quarters; 1 sweep {3,2} above
+// trial {1,0} by halves; 2 trial above sweep.
+#ifndef GYM_PRIO_MODE
+#define GYM_PRIO_MODE 0
+#endif
+template <int KIND>
+__device__ __forceinline__ void prio_start() {
+    if (GYM_PRIO_MODE == 0 || (GYM_PRIO_MODE == 1) == (KIND == 0)) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+}
+template <int KIND>
 __device__ __forceinline__ void prio_band(int done, int T) {
     asm volatile("" : "+s"(T));   // thresholds recomputed per stage (3 SALU) rather than held: no spills
-    if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
-    else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
-    else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
+    if (GYM_PRIO_MODE == 0) {
+        if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
+        else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
+        else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
+    } else {
+        const bool hi = (GYM_PRIO_MODE == 1) == (KIND == 0);
+        if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(hi ? 2 : 0);
+    }
 }
 __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "v"(v.y)); }
 
@@ -244,9 +267,9 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
     fetch(pre, 0);
     pin(pre.k0); pin(pre.k1); pin(pre.c); pin(pre.u0);
-    prio_start();
+    prio_start<1>();
     for (int t = 0; t < T; ++t) {
-        prio_band(t, T);
+        prio_band<1>(t, T);
         const double2 k0 = pre.k0, k1 = pre.k1, c = pre.c;
         const double u0 = pre.u0;
         if (t + 1 < T) fetch(pre, t + 1);
@@ -435,18 +458,18 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         if (!U0Z) pu0 = bld1(rU, o1, 0);
     }
     pin(pa); pin(pb); pin(pu0); pin(pu1);
-    prio_start();
+    prio_start<0>();
     for (int t = T - 1; t >= 0; --t) {
-        prio_band(T - 1 - t, T);
+        prio_band<0>(T - 1 - t, T);
         const double2 xa = pa, xb = pb;
         const double ut0 = pu0, ut1 = pu1;
         if (t > 0) {
             const auto rX = rsrc(Xb + (int64_t)(t - 1) * (2 * (int64_t)row));
             const auto rU = rsrc(Ub + (int64_t)(t - 1) * row);
-            pa = bld2(rX, o2, 0);
-            pb = bld2(rX, o2, row);
-            if (!U0Z) pu0 = bld1(rU, o1, 0);
-            pu1 = bld1(rU, o1, plane);
+            pa = bld2<SW_LD>(rX, o2, 0);
+            pb = bld2<SW_LD>(rX, o2, row);
+            if (!U0Z) pu0 = bld1<SW_LD>(rU, o1, 0);
+            pu1 = bld1<SW_LD>(rU, o1, plane);
         }
         double k0, k1, k2, k3, s0, s1;
 #ifndef GYM_NO_KARG
@@ -457,10 +480,77 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
 #endif
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        bst2(rK, o2, 0, k0, k1);
-        bst2(rK, o2, row, k2, k3);
-        bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+        bst2<SW_ST>(rK, o2, 0, k0, k1);
+        bst2<SW_ST>(rK, o2, row, k2, k3);
+        bst2<SW_ST>(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
     }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// Solver sweep with a prefetch distance of two stages (three register sets A, B, C, loop unrolled by 3):
+// each set is refilled right after its stage has consumed it, so a load is issued two stages before its
+// use with no register rotation (a rotated set would have to wait for its load before the copy).  The
+// sweep's stage is shorter than the trial's (332 vs ~430 VALU), so one stage of cover leaves it waiting
+// on HBM whenever the loaded latency exceeds one stage -- on some boxes the serial sweep ran 50% longer
+// than the trial over the same bytes.
+struct SwStage {
+    double2 a, b;
+    double u0, u1;
+};
+
+template <bool U0Z>
+__device__ __forceinline__ void backward_solver_lane_deep(const Dyn& m, const KW& w,
+                                                          const double2* __restrict__ x, const double* __restrict__ u,
+                                                          const double* __restrict__ xr, const double* __restrict__ ur,
+                                                          double2* __restrict__ K1, double2* __restrict__ cs,
+                                                          int64_t l, int64_t Bp, int N, double& dJ_out,
+                                                          double& smax_out) {
+    const int T = N - 1;
+    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Xb = reinterpret_cast<const char*>(x);
+    const char* Ub = reinterpret_cast<const char*>(u);
+    const char* Kb = reinterpret_cast<const char*>(K1);
+    const char* Cb = reinterpret_cast<const char*>(cs);
+    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    auto fetch = [&](SwStage& q, int t) {
+        if (t < 0) return;   // (wave-uniform)
+        const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row));
+        const auto rU = rsrc(Ub + (int64_t)t * row);
+        q.a = bld2<SW_LD>(rX, o2, 0);
+        q.b = bld2<SW_LD>(rX, o2, row);
+        q.u0 = U0Z ? 0.0 : bld1<SW_LD>(rU, o1, 0);
+        q.u1 = bld1<SW_LD>(rU, o1, plane);
+    };
+    auto stage = [&](const SwStage& q, int t) {
+        prio_band<0>(T - 1 - t, T);
+        double k0, k1, k2, k3, s0, s1;
+        const KArgs ka = kernarg_consts();
+        S.step(ka.m, ka.w, q.a, q.b, q.u0, q.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
+        const double c1 = q.u1 - (((k0 * q.a.x + k1 * q.a.y) + k2 * q.b.x) + k3 * q.b.y);
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        bst2<SW_ST>(rK, o2, 0, k0, k1);
+        bst2<SW_ST>(rK, o2, row, k2, k3);
+        bst2<SW_ST>(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+    };
+    SwStage A, B, C;   // sets of stages < 0 are never read
+    fetch(A, T - 1); fetch(B, T - 2); fetch(C, T - 3);
+    pin(A.a); pin(A.b); pin(A.u1); pin(B.a); pin(B.b); pin(B.u1); pin(C.a); pin(C.b); pin(C.u1);
+    if (!U0Z) { pin(A.u0); pin(B.u0); pin(C.u0); }
+    prio_start<0>();
+    int t = T - 1;
+    for (; t >= 2; t -= 3) {
+        stage(A, t);     fetch(A, t - 3);
+        __builtin_amdgcn_sched_barrier(0);   // keep the unrolled stages apart (register pressure)
+        stage(B, t - 1); fetch(B, t - 4);
+        __builtin_amdgcn_sched_barrier(0);
+        stage(C, t - 2); fetch(C, t - 5);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t >= 0) stage(A, t);
+    if (t >= 1) stage(B, t - 1);
     dJ_out = S.dJ;
     smax_out = S.smax;
 }
@@ -517,11 +607,11 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
         const int c0 = (nblk - 1) * CKI;
         fetch(q, c0, T - c0);
     }
-    prio_start();
+    prio_start<0>();
     for (int bk = nblk - 1; bk >= 0; --bk) {
         const int c0 = bk * CKI;
         const int len = (T - c0 < CKI) ? T - c0 : CKI;
-        prio_band(T - c0 - len, T);
+        prio_band<0>(T - c0 - len, T);
         // knots c0 .. c0+len-1 into LDS: the checkpoint, then the trial's x_{t+1} = RK4(x_t, u1_t); the
         // block's controls too, so that no register holds them across the stages
         {
@@ -975,7 +1065,11 @@ __device__ __forceinline__ void backward_solver(const Dyn& m, const KW& w, const
     if (CK)
         backward_solver_lane_ck<U0Z>(m, w, x, u, xr, ur, K1, cs, lds, l, Bp, N, d, s);
     else
+#ifdef GYM_SWEEP_DEEP
+        backward_solver_lane_deep<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
+#else
         backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
+#endif
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;

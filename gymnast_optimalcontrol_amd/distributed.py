@@ -30,16 +30,27 @@ def env_rank_world() -> tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def local_device_index(local_rank: int) -> int:
+    """This rank's GPU: local_rank, wrapped onto the visible devices (one process per GPU on a full node; a
+    multi-rank rehearsal on fewer GPUs shares them)."""
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return local_rank % n if n else 0
+
+
 def init_process_group(backend: str | None = None):
-    """Initialise torch.distributed from the environment if WORLD_SIZE > 1 (RCCL on GPUs, gloo on CPU)."""
+    """Initialise torch.distributed from the environment if WORLD_SIZE > 1 (RCCL on GPUs, gloo on CPU).
+
+    GYM_DIST_BACKEND overrides the backend (e.g. gloo to rehearse several ranks on one GPU: RCCL refuses two
+    ranks on the same device)."""
     rank, local_rank, world = env_rank_world()
     if world > 1 and not dist.is_initialized():
+        backend = backend or os.environ.get("GYM_DIST_BACKEND")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
-            torch.cuda.set_device(local_rank)
+            torch.cuda.set_device(local_device_index(local_rank))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kw = {"device_id": torch.device("cuda", local_rank)} if backend == "nccl" else {}
+        kw = {"device_id": torch.device("cuda", local_device_index(local_rank))} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, local_rank, world
 
