@@ -106,13 +106,6 @@ __device__ __forceinline__ void st_nt(double* p, double a) { __builtin_nontempor
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 constexpr int kNT = 2;  // gfx950 cache-policy bits: nt (streamed once)
-#ifndef GYM_SW_LD
-#define GYM_SW_LD 2
-#endif
-#ifndef GYM_SW_ST
-#define GYM_SW_ST 2
-#endif
-constexpr int SW_LD = GYM_SW_LD, SW_ST = GYM_SW_ST;   // the solver sweep's load / store policies
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
@@ -140,27 +133,16 @@ __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 // / 2.49 ms of a 2.5 ms launch), so the launch ends with one wave per SIMD and few loads in flight.  With
 // the bands the lagging waves win arbitration, all finish together, and the launch is 6% shorter.
 // The stage index is wave-uniform: these are scalar compares and s_setprio, no VALU.
-// KIND: 0 = sweep, 1 = trial.  GYM_PRIO_MODE (experiments): 0 both 3..0 by quarters; 1 sweep {3,2} above
-// trial {1,0} by halves; 2 trial above sweep.
-#ifndef GYM_PRIO_MODE
-#define GYM_PRIO_MODE 0
-#endif
+// KIND: 0 = sweep, 1 = trial.  (Measured alternatives: sweep banded above the trial, 1.3% slower; trial above
+// the sweep, 9.6% slower.)
 template <int KIND>
-__device__ __forceinline__ void prio_start() {
-    if (GYM_PRIO_MODE == 0 || (GYM_PRIO_MODE == 1) == (KIND == 0)) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(1);
-}
+__device__ __forceinline__ void prio_start() { __builtin_amdgcn_s_setprio(3); }
 template <int KIND>
 __device__ __forceinline__ void prio_band(int done, int T) {
     asm volatile("" : "+s"(T));   // thresholds recomputed per stage (3 SALU) rather than held: no spills
-    if (GYM_PRIO_MODE == 0) {
-        if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
-        else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
-        else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
-    } else {
-        const bool hi = (GYM_PRIO_MODE == 1) == (KIND == 0);
-        if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(hi ? 2 : 0);
-    }
+    if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
+    else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
+    else if (done >= (T >> 2)) __builtin_amdgcn_s_setprio(2);
 }
 __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "v"(v.y)); }
 
@@ -279,14 +261,9 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
         const double v1 = (c.x + kx) + gamma * c.y;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
-#ifndef GYM_NO_KARG
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
         J += xcost(ka.w.Q, n0, n1, n2, n3, xr + 4 * t);
         J += f0 * (ka.w.R[0] * f0) + f1 * (ka.w.R[1] * f1);
-#else
-        J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
-        J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
-#endif
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
             if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
@@ -466,91 +443,20 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         if (t > 0) {
             const auto rX = rsrc(Xb + (int64_t)(t - 1) * (2 * (int64_t)row));
             const auto rU = rsrc(Ub + (int64_t)(t - 1) * row);
-            pa = bld2<SW_LD>(rX, o2, 0);
-            pb = bld2<SW_LD>(rX, o2, row);
-            if (!U0Z) pu0 = bld1<SW_LD>(rU, o1, 0);
-            pu1 = bld1<SW_LD>(rU, o1, plane);
+            pa = bld2(rX, o2, 0);
+            pb = bld2(rX, o2, row);
+            if (!U0Z) pu0 = bld1(rU, o1, 0);
+            pu1 = bld1(rU, o1, plane);
         }
         double k0, k1, k2, k3, s0, s1;
-#ifndef GYM_NO_KARG
         const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
         S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
-#else
-        S.step(m, w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
-#endif
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        bst2<SW_ST>(rK, o2, 0, k0, k1);
-        bst2<SW_ST>(rK, o2, row, k2, k3);
-        bst2<SW_ST>(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+        bst2(rK, o2, 0, k0, k1);
+        bst2(rK, o2, row, k2, k3);
+        bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
     }
-    dJ_out = S.dJ;
-    smax_out = S.smax;
-}
-
-// Solver sweep with a prefetch distance of two stages (three register sets A, B, C, loop unrolled by 3):
-// each set is refilled right after its stage has consumed it, so a load is issued two stages before its
-// use with no register rotation (a rotated set would have to wait for its load before the copy).  The
-// sweep's stage is shorter than the trial's (332 vs ~430 VALU), so one stage of cover leaves it waiting
-// on HBM whenever the loaded latency exceeds one stage -- on some boxes the serial sweep ran 50% longer
-// than the trial over the same bytes.
-struct SwStage {
-    double2 a, b;
-    double u0, u1;
-};
-
-template <bool U0Z>
-__device__ __forceinline__ void backward_solver_lane_deep(const Dyn& m, const KW& w,
-                                                          const double2* __restrict__ x, const double* __restrict__ u,
-                                                          const double* __restrict__ xr, const double* __restrict__ ur,
-                                                          double2* __restrict__ K1, double2* __restrict__ cs,
-                                                          int64_t l, int64_t Bp, int N, double& dJ_out,
-                                                          double& smax_out) {
-    const int T = N - 1;
-    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
-    const char* Xb = reinterpret_cast<const char*>(x);
-    const char* Ub = reinterpret_cast<const char*>(u);
-    const char* Kb = reinterpret_cast<const char*>(K1);
-    const char* Cb = reinterpret_cast<const char*>(cs);
-    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
-    const gym::PolyRegs pk = gym::poly_vgprs();
-    auto fetch = [&](SwStage& q, int t) {
-        if (t < 0) return;   // (wave-uniform)
-        const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row));
-        const auto rU = rsrc(Ub + (int64_t)t * row);
-        q.a = bld2<SW_LD>(rX, o2, 0);
-        q.b = bld2<SW_LD>(rX, o2, row);
-        q.u0 = U0Z ? 0.0 : bld1<SW_LD>(rU, o1, 0);
-        q.u1 = bld1<SW_LD>(rU, o1, plane);
-    };
-    auto stage = [&](const SwStage& q, int t) {
-        prio_band<0>(T - 1 - t, T);
-        double k0, k1, k2, k3, s0, s1;
-        const KArgs ka = kernarg_consts();
-        S.step(ka.m, ka.w, q.a, q.b, q.u0, q.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
-        const double c1 = q.u1 - (((k0 * q.a.x + k1 * q.a.y) + k2 * q.b.x) + k3 * q.b.y);
-        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        bst2<SW_ST>(rK, o2, 0, k0, k1);
-        bst2<SW_ST>(rK, o2, row, k2, k3);
-        bst2<SW_ST>(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
-    };
-    SwStage A, B, C;   // sets of stages < 0 are never read
-    fetch(A, T - 1); fetch(B, T - 2); fetch(C, T - 3);
-    pin(A.a); pin(A.b); pin(A.u1); pin(B.a); pin(B.b); pin(B.u1); pin(C.a); pin(C.b); pin(C.u1);
-    if (!U0Z) { pin(A.u0); pin(B.u0); pin(C.u0); }
-    prio_start<0>();
-    int t = T - 1;
-    for (; t >= 2; t -= 3) {
-        stage(A, t);     fetch(A, t - 3);
-        __builtin_amdgcn_sched_barrier(0);   // keep the unrolled stages apart (register pressure)
-        stage(B, t - 1); fetch(B, t - 4);
-        __builtin_amdgcn_sched_barrier(0);
-        stage(C, t - 2); fetch(C, t - 5);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (t >= 0) stage(A, t);
-    if (t >= 1) stage(B, t - 1);
     dJ_out = S.dJ;
     smax_out = S.smax;
 }
@@ -1065,11 +971,7 @@ __device__ __forceinline__ void backward_solver(const Dyn& m, const KW& w, const
     if (CK)
         backward_solver_lane_ck<U0Z>(m, w, x, u, xr, ur, K1, cs, lds, l, Bp, N, d, s);
     else
-#ifdef GYM_SWEEP_DEEP
-        backward_solver_lane_deep<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
-#else
         backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
-#endif
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
