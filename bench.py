@@ -155,7 +155,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="lanes per GPU (weak scaling); default 262144 (newton, cfg 3) or 8192 (mpc, cfg 5)")
     ap.add_argument("--max-iters", type=int, default=5000)
-    ap.add_argument("--cpu-lanes", type=int, default=512)
+    ap.add_argument("--cpu-lanes", type=int, default=4096,
+                    help="lanes of the bounded CPU-baseline sample (about 10 s on 16 host cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--sync-every", type=int, default=4,

@@ -146,8 +146,19 @@ __device__ __forceinline__ void prio_band(int done, int T) {
 }
 __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "v"(v.y)); }
 
-// element index of (t, component-group p of P, lane) in a time-major SoA stream
+// element index of (t, row p of P, lane) in a time-major plane stream (W = 1 doubles): (L, P, Bp)
 __device__ __forceinline__ int64_t pix(int t, int p, int P, int64_t l, int64_t Bp) { return ((int64_t)t * P + p) * Bp + l; }
+// element index of (t, row p of P, lane) in a wave-blocked pair stream (W = 2, double2): (L, Bp/64, P, 64), i.e.
+// the P rows of one wavefront's 64 lanes at one stage form one contiguous P KiB block (one DRAM burst sequence
+// instead of P 1-KiB pieces Bp*16 bytes apart).  The stage stride is P*Bp elements, as for planes.
+__device__ __forceinline__ int64_t wix(int64_t t, int p, int P, int64_t l, int64_t Bp) {
+    return t * P * Bp + (l & ~(int64_t)(BLK - 1)) * P + p * BLK + (l & (BLK - 1));
+}
+// the same as a byte offset within one stage (buffer-resource addressing), and the row-to-row step
+__device__ __forceinline__ uint32_t wbo(int64_t l, int P) {
+    return (uint32_t)(((l & ~(int64_t)(BLK - 1)) * P + (l & (BLK - 1))) * 16);
+}
+constexpr uint32_t WROW = BLK * 16;
 
 // stage cost exactly as total_cost accumulates it (:244-245): J += dx^T Q dx ; J += du^T R du
 __device__ __forceinline__ double xcost(const double* w, double n0, double n1, double n2, double n3,
@@ -172,15 +183,15 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const KW& w, const d
     const int T = N - 1;
     double J = 0.0;
     if (WRITE) {
-        xn[l] = make_double2(n0, n1);
-        xn[Bp + l] = make_double2(n2, n3);
+        xn[wix(0, 0, 2, l, Bp)] = make_double2(n0, n1);
+        xn[wix(0, 1, 2, l, Bp)] = make_double2(n2, n3);
     }
     for (int t = 0; t < T; ++t) {
         double v0 = u[pix(t, 0, 2, l, Bp)], v1 = u[pix(t, 1, 2, l, Bp)];
         if (FULLK) {
-            const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
-            const double2 k0 = K[pix(t, 0, 4, l, Bp)], k1 = K[pix(t, 1, 4, l, Bp)];
-            const double2 k2 = K[pix(t, 2, 4, l, Bp)], k3 = K[pix(t, 3, 4, l, Bp)];
+            const double2 a = x[wix(t, 0, 2, l, Bp)], b = x[wix(t, 1, 2, l, Bp)];
+            const double2 k0 = K[wix(t, 0, 4, l, Bp)], k1 = K[wix(t, 1, 4, l, Bp)];
+            const double2 k2 = K[wix(t, 2, 4, l, Bp)], k3 = K[wix(t, 3, 4, l, Bp)];
             const double d0 = n0 - a.x, d1 = n1 - a.y, d2 = n2 - b.x, d3 = n3 - b.y;
             const double kd0 = ((k0.x * d0 + k0.y * d1) + k1.x * d2) + k1.y * d3;
             const double kd1 = ((k2.x * d0 + k2.y * d1) + k3.x * d2) + k3.y * d3;
@@ -197,8 +208,8 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const KW& w, const d
         J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
         gym::rk4(m, n0, n1, n2, n3, v1);
         if (WRITE) {
-            xn[pix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
-            xn[pix(t + 1, 1, 2, l, Bp)] = make_double2(n2, n3);
+            xn[wix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
+            xn[wix(t + 1, 1, 2, l, Bp)] = make_double2(n2, n3);
         }
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
@@ -225,7 +236,8 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
                                                 double n3) {
     const int T = N - 1;
     const double G00 = w.G00, iG00 = w.iG00;
-    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;   // lane byte offsets (pairs, planes)
+    // lane byte offsets: 2-row wave-blocked pairs (K1, x), 1-row pairs (cs), planes (u)
+    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Kb = reinterpret_cast<const char*>(K1);   // stage stride 2 rows
     const char* Cb = reinterpret_cast<const char*>(cs);   // stage stride 1 row
@@ -236,13 +248,13 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     if (WRITE) {
         const auto rX = rsrc(Xb);
         bst2(rX, o2, 0, n0, n1);
-        bst2(rX, o2, row, n2, n3);
+        bst2(rX, o2, WROW, n2, n3);
     }
     auto fetch = [&](TrialStage& q, int t) {   // stage t's streams into register set q
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         q.k0 = bld2<CP>(rK, o2, 0);
-        q.k1 = bld2<CP>(rK, o2, row);
-        q.c = bld2<CP>(rsrc(Cb + (int64_t)t * row), o2, 0);
+        q.k1 = bld2<CP>(rK, o2, WROW);
+        q.c = bld2<CP>(rsrc(Cb + (int64_t)t * row), o2c, 0);
         q.u0 = U0Z ? 0.0 : bld1<CP>(rsrc(Ub + (int64_t)t * row), o1, 0);
     };
     const gym::PolyRegs pk = gym::poly_vgprs();   // loop-invariant coefficients held in VGPRs
@@ -273,7 +285,7 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
             bst2(rX, o2, 0, n0, n1);
-            bst2(rX, o2, row, n2, n3);
+            bst2(rX, o2, WROW, n2, n3);
         }
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
@@ -378,30 +390,30 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const d
                                               double* __restrict__ sig, double2* __restrict__ lam, int64_t l,
                                               int64_t Bp, int N, double& dJ_out, double& smax_out) {
     const int T = N - 1;
-    Sweep<LAMBDA> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    Sweep<LAMBDA> S(w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     if (LAMBDA) {
-        lam[pix(T, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
-        lam[pix(T, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
+        lam[wix(T, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
+        lam[wix(T, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
     }
-    double2 pa = x[pix(T - 1, 0, 2, l, Bp)], pb = x[pix(T - 1, 1, 2, l, Bp)];
+    double2 pa = x[wix(T - 1, 0, 2, l, Bp)], pb = x[wix(T - 1, 1, 2, l, Bp)];
     double pu0 = u[pix(T - 1, 0, 2, l, Bp)], pu1 = u[pix(T - 1, 1, 2, l, Bp)];
     for (int t = T - 1; t >= 0; --t) {
         const double2 xa = pa, xb = pb;
         const double ut0 = pu0, ut1 = pu1;
         if (t > 0) {
-            pa = x[pix(t - 1, 0, 2, l, Bp)];
-            pb = x[pix(t - 1, 1, 2, l, Bp)];
+            pa = x[wix(t - 1, 0, 2, l, Bp)];
+            pb = x[wix(t - 1, 1, 2, l, Bp)];
             pu0 = u[pix(t - 1, 0, 2, l, Bp)];
             pu1 = u[pix(t - 1, 1, 2, l, Bp)];
         }
         double k0, k1, k2, k3, s0, s1;
         S.step(m, w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
         if (LAMBDA) {
-            lam[pix(t, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
-            lam[pix(t, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
+            lam[wix(t, 0, 2, l, Bp)] = make_double2(S.l0, S.l1);
+            lam[wix(t, 1, 2, l, Bp)] = make_double2(S.l2, S.l3);
         }
-        K1[pix(t, 0, 2, l, Bp)] = make_double2(k0, k1);
-        K1[pix(t, 1, 2, l, Bp)] = make_double2(k2, k3);
+        K1[wix(t, 0, 2, l, Bp)] = make_double2(k0, k1);
+        K1[wix(t, 1, 2, l, Bp)] = make_double2(k2, k3);
         sig[pix(t, 0, 2, l, Bp)] = s0;
         sig[pix(t, 1, 2, l, Bp)] = s1;
     }
@@ -419,19 +431,20 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
                                                      double2* __restrict__ K1, double2* __restrict__ cs, int64_t l,
                                                      int64_t Bp, int N, double& dJ_out, double& smax_out) {
     const int T = N - 1;
-    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;   // lane byte offsets (pairs, planes)
+    // lane byte offsets: 2-row wave-blocked pairs (x, K1), 1-row pairs (cs), planes (u)
+    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Xb = reinterpret_cast<const char*>(x);    // stage stride 2 rows
     const char* Ub = reinterpret_cast<const char*>(u);    // stage stride 1 row
     const char* Kb = reinterpret_cast<const char*>(K1);
     const char* Cb = reinterpret_cast<const char*>(cs);
-    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    Sweep<false> S(w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     const gym::PolyRegs pk = gym::poly_vgprs();
     double2 pa, pb;
     double pu0 = 0.0, pu1;
     {
         const auto rX = rsrc(Xb + (int64_t)(T - 1) * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)(T - 1) * row);
-        pa = bld2(rX, o2, 0); pb = bld2(rX, o2, row); pu1 = bld1(rU, o1, plane);
+        pa = bld2(rX, o2, 0); pb = bld2(rX, o2, WROW); pu1 = bld1(rU, o1, plane);
         if (!U0Z) pu0 = bld1(rU, o1, 0);
     }
     pin(pa); pin(pb); pin(pu0); pin(pu1);
@@ -444,7 +457,7 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
             const auto rX = rsrc(Xb + (int64_t)(t - 1) * (2 * (int64_t)row));
             const auto rU = rsrc(Ub + (int64_t)(t - 1) * row);
             pa = bld2(rX, o2, 0);
-            pb = bld2(rX, o2, row);
+            pb = bld2(rX, o2, WROW);
             if (!U0Z) pu0 = bld1(rU, o1, 0);
             pu1 = bld1(rU, o1, plane);
         }
@@ -454,8 +467,8 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         bst2(rK, o2, 0, k0, k1);
-        bst2(rK, o2, row, k2, k3);
-        bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+        bst2(rK, o2, WROW, k2, k3);
+        bst2(rsrc(Cb + (int64_t)t * row), o2c, 0, c1, s1);
     }
     dJ_out = S.dJ;
     smax_out = S.smax;
@@ -482,7 +495,7 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
                                                         double2* __restrict__ lds, int64_t l, int64_t Bp, int N,
                                                         double& dJ_out, double& smax_out) {
     const int T = N - 1;
-    const uint32_t o2 = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Xb = reinterpret_cast<const char*>(x);
     const char* Ub = reinterpret_cast<const char*>(u);
@@ -491,11 +504,11 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
     const int ln = threadIdx.x;
     double* lu1 = reinterpret_cast<double*>(lds + 2 * CKI * BLK);   // (CKI, 64) tau2 controls
     double* lu0 = lu1 + CKI * BLK;                                   // (CKI, 64) tau1 controls (!U0Z)
-    Sweep<false> S(w, x[pix(T, 0, 2, l, Bp)], x[pix(T, 1, 2, l, Bp)], xr + 4 * T);
+    Sweep<false> S(w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     auto fetch = [&](CkBlock& q, int c0, int len) {
         const auto rX = rsrc(Xb + (int64_t)c0 * (2 * (int64_t)row));
         q.a = bld2(rX, o2, 0);
-        q.b = bld2(rX, o2, row);
+        q.b = bld2(rX, o2, WROW);
 #pragma unroll
         for (int j = 0; j < CKI; ++j) {
             q.u0[j] = 0.0;
@@ -553,8 +566,8 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
                 const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
                 const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
                 bst2(rK, o2, 0, k0, k1);
-                bst2(rK, o2, row, k2, k3);
-                bst2(rsrc(Cb + (int64_t)t * row), o2, 0, c1, s1);
+                bst2(rK, o2, WROW, k2, k3);
+                bst2(rsrc(Cb + (int64_t)t * row), o2c, 0, c1, s1);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -602,7 +615,7 @@ __global__ __launch_bounds__(BLK) void k_closed_loop(Dyn m, KW w, const double2*
                                                      double* __restrict__ cost, int64_t B, int64_t Bp, int N) {
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= B) return;
-    const double2 a = x[l], b = x[Bp + l];
+    const double2 a = x[wix(0, 0, 2, l, Bp)], b = x[wix(0, 1, 2, l, Bp)];
     const double J = rollout_ref<true>(m, w, x, u, Kf, s, xr, ur, xn, un, gamma[l], l, Bp, N, a.x, a.y, b.x, b.y);
     if (cost) cost[l] = J;
 }
@@ -686,13 +699,13 @@ __global__ __launch_bounds__(BLK) void k_total_cost(const double2* __restrict__ 
     if (l >= B) return;
     double J = 0.0;
     for (int t = 0; t < N - 1; ++t) {
-        const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
+        const double2 a = x[wix(t, 0, 2, l, Bp)], b = x[wix(t, 1, 2, l, Bp)];
         const double e[4] = {a.x - xr[4 * t], a.y - xr[4 * t + 1], b.x - xr[4 * t + 2], b.y - xr[4 * t + 3]};
         J += quad4(Q.v, e);
         J += quad2(R.v, u[pix(t, 0, 2, l, Bp)] - ur[2 * t], u[pix(t, 1, 2, l, Bp)] - ur[2 * t + 1]);
     }
     const int T = N - 1;
-    const double2 a = x[pix(T, 0, 2, l, Bp)], b = x[pix(T, 1, 2, l, Bp)];
+    const double2 a = x[wix(T, 0, 2, l, Bp)], b = x[wix(T, 1, 2, l, Bp)];
     const double e[4] = {a.x - xr[4 * T], a.y - xr[4 * T + 1], b.x - xr[4 * T + 2], b.y - xr[4 * T + 3]};
     cost[l] = J + quad4(QT.v, e);
 }
@@ -709,7 +722,7 @@ __global__ __launch_bounds__(BLK) void k_linearize(Dyn m, KW w, const double2* _
     const double dt = m.h;
     const int T = N - 1;
     for (int t = 0; t < T; ++t) {
-        const double2 a = x[pix(t, 0, 2, l, Bp)], b = x[pix(t, 1, 2, l, Bp)];
+        const double2 a = x[wix(t, 0, 2, l, Bp)], b = x[wix(t, 1, 2, l, Bp)];
         const double v0 = u[pix(t, 0, 2, l, Bp)], v1 = u[pix(t, 1, 2, l, Bp)];
         const gym::Jac J = gym::jacobian(m, a.x, a.y, b.x, b.y, v1);
         double A[16] = {1.0, 0.0, dt, 0.0, 0.0, 1.0, 0.0, dt};
@@ -729,7 +742,7 @@ __global__ __launch_bounds__(BLK) void k_linearize(Dyn m, KW w, const double2* _
         r[((int64_t)t * 2) * Bp + l] = (2.0 * w.R[0]) * (v0 - ur[2 * t]);
         r[((int64_t)t * 2 + 1) * Bp + l] = (2.0 * w.R[1]) * (v1 - ur[2 * t + 1]);
     }
-    const double2 a = x[pix(T, 0, 2, l, Bp)], b = x[pix(T, 1, 2, l, Bp)];
+    const double2 a = x[wix(T, 0, 2, l, Bp)], b = x[wix(T, 1, 2, l, Bp)];
     const double xe[4] = {a.x - xr[4 * T], a.y - xr[4 * T + 1], b.x - xr[4 * T + 2], b.y - xr[4 * T + 3]};
 #pragma unroll
     for (int c = 0; c < 4; ++c) qT[(int64_t)c * Bp + l] = (2.0 * w.QT[c]) * xe[c];
@@ -873,7 +886,8 @@ __global__ void k_pack(const double* __restrict__ src, double* __restrict__ dst,
     const int p = (int)(rest % P);
     const int64_t t = rest / P;
     const double* s = src + (lane * L + t) * C + W * p;
-    for (int k = 0; k < W; ++k) dst[W * i + k] = (lane < B) ? s[k] : 0.0;
+    const int64_t d = W == 2 ? wix(t, p, P, lane, Bp) : i;   // pairs: wave-blocked
+    for (int k = 0; k < W; ++k) dst[W * d + k] = (lane < B) ? s[k] : 0.0;
 }
 
 __global__ void k_unpack(const double* __restrict__ s0, const double* __restrict__ s1,
@@ -887,7 +901,7 @@ __global__ void k_unpack(const double* __restrict__ s0, const double* __restrict
     const int64_t t = rest % L;
     const int64_t lane = rest / L;
     const double* s = (sel && sel[lane]) ? s1 : s0;
-    const double* e = s + W * ((t * P + p) * Bp + lane);
+    const double* e = s + W * (W == 2 ? wix(t, p, P, lane, Bp) : (t * P + p) * Bp + lane);
     for (int k = 0; k < W; ++k) dst[W * o + k] = e[k];
 }
 
@@ -896,7 +910,7 @@ __global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restric
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (lane, t)
     if (o >= B * T) return;
     const int64_t t = o % T, lane = o / T;
-    const double2 a = K1[pix((int)t, 0, 2, lane, Bp)], b = K1[pix((int)t, 1, 2, lane, Bp)];
+    const double2 a = K1[wix(t, 0, 2, lane, Bp)], b = K1[wix(t, 1, 2, lane, Bp)];
     double* d = K + 8 * o;
     d[0] = 0.0; d[1] = 0.0; d[2] = 0.0; d[3] = 0.0;
     d[4] = a.x; d[5] = a.y; d[6] = b.x; d[7] = b.y;
@@ -1034,7 +1048,7 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const So
                                              int32_t* __restrict__ res_buf, int32_t* __restrict__ n_roll,
                                              int32_t* __restrict__ retry_list, int32_t* __restrict__ counter,
                                              double* __restrict__ hist_cost, int64_t l, int64_t Bp, int N) {
-    const double2 xa = io.x[l], xb = io.x[Bp + l];
+    const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
     const double g = a.gamma0;
     const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
                                                    xa.y, xb.x, xb.y);
@@ -1114,7 +1128,7 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a,
         const int64_t l = retry_list[r];
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
-        const double2 xa = io.x[l], xb = io.x[Bp + l];
+        const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
         const double Jn = rollout_cform<false, U0Z>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x,
                                                     xa.y, xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
@@ -1149,7 +1163,7 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
         n_roll[l] += jacc;
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
-        const double2 xa = io.x[l], xb = io.x[Bp + l];
+        const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
         const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
                                                        xa.y, xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
@@ -1185,7 +1199,7 @@ __global__ __launch_bounds__(BLK) void k_gamma_sweep(Dyn m, KW w, const double2*
         cost_out[(int64_t)g * Bp + l] = __builtin_nan("");
         return;
     }
-    const double2 a = x[l], b = x[Bp + l];
+    const double2 a = x[wix(0, 0, 2, l, Bp)], b = x[wix(0, 1, 2, l, Bp)];
     cost_out[(int64_t)g * Bp + l] = rollout_ref<true, false>(m, w, x, u, Kf, sig, xr, ur, nullptr, nullptr, gammas[g],
                                                              l, Bp, N, a.x, a.y, b.x, b.y);
 }
@@ -1208,7 +1222,7 @@ __global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const doubl
         cost_out[(int64_t)g * Bp + l] = __builtin_nan("");
         return;
     }
-    const double2 a = x[l], b = x[Bp + l];
+    const double2 a = x[wix(0, 0, 2, l, Bp)], b = x[wix(0, 1, 2, l, Bp)];
     cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, false, 0>(m, w, u, K1, cs, xr, ur, nullptr, nullptr,
                                                                         gammas[g], l, Bp, N, a.x, a.y, b.x, b.y);
 }
@@ -1319,12 +1333,12 @@ __global__ __launch_bounds__(BLK) void k_fill_states(Dyn m, double2* __restrict_
     const int sel = sel_buf >= 0 ? sel_buf : res_buf[l];
     double2* xs = sel ? x1b : x0b;
     const double* us = sel ? u1b : u0b;
-    const double2 a = xs[l], b = xs[Bp + l];
+    const double2 a = xs[wix(0, 0, 2, l, Bp)], b = xs[wix(0, 1, 2, l, Bp)];
     double n0 = a.x, n1 = a.y, n2 = b.x, n3 = b.y;
     for (int t = 0; t < N - 1; ++t) {
         gym::rk4(m, n0, n1, n2, n3, us[pix(t, 1, 2, l, Bp)]);
-        st_nt(xs + pix(t + 1, 0, 2, l, Bp), n0, n1);
-        st_nt(xs + pix(t + 1, 1, 2, l, Bp), n2, n3);
+        st_nt(xs + wix(t + 1, 0, 2, l, Bp), n0, n1);
+        st_nt(xs + wix(t + 1, 1, 2, l, Bp), n2, n3);
     }
 }
 

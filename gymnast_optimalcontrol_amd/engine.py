@@ -89,7 +89,9 @@ class AcrobotEngine:
         self._w = weights.c_struct()
 
     def pack(self, a: torch.Tensor, Bp: int, W: int = 2) -> torch.Tensor:
-        """(B,L,C) lane-major -> SoA (L, C/W, Bp, W): W = 2 pairs (states, gains), W = 1 planes (controls, sigma)."""
+        """(B,L,C) lane-major -> SoA (L, C/W, Bp, W): W = 2 pairs (states, gains; wave-blocked, see the ABI header),
+        W = 1 planes (controls, sigma).  The tensor shape only sizes the buffer: pair elements are laid out as
+        (L, Bp/64, C/W, 64, 2)."""
         B, L, Cc = a.shape
         out = torch.empty((L, Cc // W, Bp, W), dtype=F64, device=self.device)
         _lib.check(self.lib.gym_pack_lanes(a.data_ptr(), out.data_ptr(), B, Bp, L, Cc, W, self.stream),

@@ -20,12 +20,15 @@
  *   lane-major  : the reference's own arrays stacked over lanes: x (B,N,4), u (B,T,2),
  *                 K (B,T,2,4), sigma (B,T,2), row-major.
  *   SoA         : time-major, lane innermost (lane stride Bp >= B, a multiple of 64):
- *     pairs  (W = 2): two fp64 components per 16-byte element, one 1 KiB load per wavefront
- *                   states   x  : (N, 2, Bp) double2   (th1, th2), (w1, w2)
- *                   gains    K1 : (T, 2, Bp) double2   row 1 of K_t (row 0 is identically 0)
- *                   gains    Kf : (T, 4, Bp) double2   full K_t: (K00,K01)(K02,K03)(K10,K11)(K12,K13)
- *                   offsets  cs : (T, Bp)    double2   (c1 = u1 - K1 x, sigma1) of the solver's sweep
- *     planes (W = 1): one component per element
+ *     pairs  (W = 2): two fp64 components per 16-byte element, one 1 KiB load per wavefront and row,
+ *                   WAVE-BLOCKED: a P-row stream is (L, Bp/64, P, 64) double2, i.e. the P rows of one
+ *                   64-lane group at one stage are one contiguous P KiB block (ABI 4; element of
+ *                   (t, row p, lane l) = t*P*Bp + (l & ~63)*P + 64 p + (l & 63))
+ *                   states   x  : (N, Bp/64, 2, 64) double2   (th1, th2), (w1, w2)
+ *                   gains    K1 : (T, Bp/64, 2, 64) double2   row 1 of K_t (row 0 is identically 0)
+ *                   gains    Kf : (T, Bp/64, 4, 64) double2   full K_t: (K00,K01)(K02,K03)(K10,K11)(K12,K13)
+ *                   offsets  cs : (T, Bp)           double2   (c1 = u1 - K1 x, sigma1) of the solver's sweep
+ *     planes (W = 1): one component per element, (L, P, Bp)
  *                   controls u  : (T, 2, Bp) double    planes tau1, tau2
  *                   sigma    s  : (T, 2, Bp) double
  */
@@ -38,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 3
+#define GYM_ABI_VERSION 4
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -104,9 +107,9 @@ typedef struct gym_batch {
     int64_t B, Bp;      /* lanes, lane stride (multiple of 64)                     */
     int32_t N, hist_len;/* knots (T = N-1); rows of the optional history buffers   */
     int32_t flags, pad; /* GYM_FLAG_*                                               */
-    double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered   */
+    double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered (wave-blocked) */
     double* u[2];       /* (T,2,Bp) control planes, double-buffered               */
-    double* K1;         /* (T,2,Bp) double2 feedback gains, row 1                 */
+    double* K1;         /* (T,2,Bp) double2 feedback gains, row 1 (wave-blocked)  */
     double* cs;         /* (T,Bp)   double2 (c1 = u1 - K1 x, sigma1) of the sweep  */
     const double* x_ref;/* (N,4) shared reference states                          */
     const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
@@ -146,7 +149,8 @@ int gym_stage_cost_derivs(const double* x, const double* xr, const double* u, co
                           const double R[4], int32_t terminal, double* l, double* gx, double* gu, int64_t n, void* stream);
 
 /* ---------------- layout transposes ---------------- */
-/* lane-major (B,L,C) -> SoA (L, C/W, Bp, W), W = 2 (pairs) or 1 (planes).  Padding lanes are zero-filled. */
+/* lane-major (B,L,C) -> SoA (L, C/W, Bp, W), W = 2 (pairs, wave-blocked) or 1 (planes).  Padding lanes are
+ * zero-filled.  Here and below "(L,P,Bp) pairs" names the wave-blocked pair layout of the Layouts note. */
 int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, int32_t W,
                    void* stream);
 /* SoA -> lane-major; if sel != NULL lane b reads from (sel[b] ? src1 : src0). */
