@@ -36,19 +36,20 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
 def algorithmic_bytes(N: int, u0_zero: bool = True) -> dict:
     """Compulsory HBM bytes per lane for one pass of each solver kernel (fp64), see DESIGN.md section 4.
 
-    backward sweep : read x (4N) + u (2T);            write K row 1 (4T) + (c1, sigma1) (2T)
-    Armijo trial   : read K row 1 (4T) + (c1, sigma1) (2T) + u0 (T) + x_0 (4);
-                     write x_new (4N) + u_new (2T)
+    backward sweep : read x (4N) + u (2T);         write K row 1 (4T) + cg (T)
+    Armijo trial   : read K row 1 (4T) + cg (T) + u0 (T) + x_0 (4);  write x_new (4N) + u_new (2T)
+    (cg = (u1 - K1 x) + gamma0 sigma1; sigma1 itself is not streamed -- the rare lanes that backtrack re-run
+    their sweep for it, which the per-launch count below does not include.)
     u0_zero (u_ref[:,0] == 0, GYM_FLAG_U0_ZERO): the tau1 plane is neither read nor written (-T on
     the sweep's reads, -T / -T on the trial's reads / writes).
-    A Newton iteration of one lane is one sweep + one trial (no backtracking): 100,096 B at N = 501,
-    88,096 B with u0_zero.  (SURVEY.md 8(d)'s 152,096 B is the reference's data flow: K stored 2x4,
+    A Newton iteration of one lane is one sweep + one trial (no backtracking): 92,096 B at N = 501,
+    80,096 B with u0_zero.  (SURVEY.md 8(d)'s 152,096 B is the reference's data flow: K stored 2x4,
     sigma stored 2-wide and the trial re-reading x and u.)
     """
     T = N - 1
     z = T if u0_zero else 0
-    bwd = 8 * (4 * N + 2 * T - z + 4 * T + 2 * T)
-    trial = 8 * (4 * T + 2 * T + (T - z) + 4 + 4 * N + 2 * T - z)
+    bwd = 8 * (4 * N + 2 * T - z + 4 * T + T)
+    trial = 8 * (4 * T + T + (T - z) + 4 + 4 * N + 2 * T - z)
     return {"backward": bwd, "trial": trial, "iteration": bwd + trial,
             "survey_per_iteration": 8 * ((4 * N + 2 * T) + 10 * T + (2 * (4 * N + 2 * T) + 10 * T))}
 

@@ -28,7 +28,7 @@ EXPORTS = (
     "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_lq_forward", "gym_track_rollout",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
-KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even")
+KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma")
 
 ABI_VERSION = 4          # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
@@ -57,7 +57,7 @@ _P = C.c_void_p
 
 
 class GymTiming(C.Structure):
-    _fields_ = [("ev", _P * 14), ("ms", C.c_double * 7), ("launches", C.c_int64 * 7), ("pending", C.c_int32),
+    _fields_ = [("ev", _P * 16), ("ms", C.c_double * 8), ("launches", C.c_int64 * 8), ("pending", C.c_int32),
                 ("pad", C.c_int32)]
 
 
@@ -94,9 +94,9 @@ _SIGS = {
     "gym_newton_phase": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_finalize": [_MP, _WP, _BP, _I32, _P, _P, _P, _P, _P],
     "gym_newton_fill_states": [_MP, _BP, _I32, _P],
-    "gym_newton_sigma": [_WP, _BP, _P, _P],
+    "gym_newton_sigma": [_MP, _WP, _BP, _P, _P],
     "gym_gamma_sweep": [_MP, _WP, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I32, _P],
-    "gym_newton_gamma_sweep": [_MP, _WP, _BP, _I32, _P, _I32, _P, _P],
+    "gym_newton_gamma_sweep": [_MP, _WP, _AP, _BP, _I32, _P, _I32, _P, _P],
     "gym_tv_lqr_gains": [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _D, _P, _P],
     "gym_dare_fixed_point": [_P, _P, _P, _P, _I32, _D, _P, _P, _P],
     "gym_lq_forward": [_P, _P, _I32, _P, _P, _I32, _D, _P, _P, _I32, _P, _P, _P],

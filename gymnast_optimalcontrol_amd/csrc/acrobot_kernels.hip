@@ -8,11 +8,13 @@
 // no LDS is needed because lanes never exchange data.
 //
 // The solver's two HBM streams per Newton iteration:
-//   backward sweep : read x (2 pairs) + u (2 planes), write K row 1 (2 pairs) + (c1, sigma1) (1 pair)
-//   Armijo trial   : read K row 1 + (c1, sigma1) + u0, write x_new (2 pairs) + u_new (2 planes)
-// where c1 = u1 - K1 x folds the reference's u1 + K1 (x_new - x) into c1 + K1 x_new, so the trial
-// never re-reads the old trajectory x; sigma0 = -r0 / (2 R0) is recomputed from u0 bit-identically.
-// Streamed once per pass, these use non-temporal loads/stores.
+//   backward sweep : read x (2 pairs) + u (2 planes), write K row 1 (2 pairs) + cg (1 plane)
+//   Armijo trial   : read K row 1 + cg + u0, write x_new (2 pairs) + u_new (2 planes)
+// where cg = (u1 - K1 x) + gamma0 sigma1 folds the reference's u1 + K1 (x_new - x) + gamma0 sigma1 into
+// cg + K1 x_new, so the first trial never re-reads the old trajectory x nor sigma1; sigma0 = -r0 / (2R0) is
+// recomputed from u0 bit-identically.  sigma1 itself is not streamed: the rare consumers (trials 2..20 of
+// lanes that backtrack, the final sigma output, gamma sweeps) re-run the lane's sweep, which reproduces it
+// bit for bit, into the sigma1 plane.  Streamed once per pass, these use non-temporal loads/stores.
 //
 // Reference: /root/reference/trajectory_generation.py (newton_Algorithm :298-398 and the
 // primitives it calls) and dynamics.py.  See include/gymnast_acrobot.h for the ABI.
@@ -218,29 +220,34 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const KW& w, const d
 // ------------------------------------------------------------------------------------------
 // Solver rollout (Armijo trial / candidate / accepted-candidate re-run), offset form:
 //   u_new0 = u0 + gamma sigma0,  sigma0 = -(2R0 (u0 - ur0)) / (2R0)     (bit-identical to the sweep)
-//   u_new1 = (c1 + K1 x_new) + gamma sigma1,  c1 = u1 - K1 x  (the sweep's offset)
-// Streams per stage: K1 (2 pairs) + (c1, sigma1) (1 pair) + u0 (plane) in; x_new, u_new out.
+//   u_new1 = cg + K1 x_new,  cg = (u1 - K1 x) + gamma0 sigma1  (the sweep's offset)          first trial
+//   u_new1 = fma(gamma - gamma0, sigma1, cg + K1 x_new)                          SIG: any other step size
+// (at gamma = gamma0 the SIG form returns the first trial's value exactly).
+// Streams per stage: K1 (2 pairs) + cg (plane) [+ sigma1 (plane) if SIG] + u0 (plane) in; x_new, u_new out.
+// cs: (T, 2, Bp) planes, plane 0 = cg, plane 1 = sigma1.
 // ------------------------------------------------------------------------------------------
 // Streams of one stage of the offset-form rollout, prefetched into registers one stage ahead.
 struct TrialStage {
-    double2 k0, k1, c;   // K row 1 (two pairs), (c1, sigma1)
+    double2 k0, k1;      // K row 1 (two pairs)
+    double cg, s1;       // offset cg, sigma1 (SIG only)
     double u0;           // tau1 control (0 when U0Z)
 };
 
-template <bool WRITE, bool U0Z, bool CK = false, int CP = kNT>
+template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT>
 __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const double* __restrict__ u,
-                                                const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                const double2* __restrict__ K1, const double* __restrict__ cs,
                                                 const double* __restrict__ xr, const double* __restrict__ ur,
                                                 double2* __restrict__ xn, double* __restrict__ un, double gamma,
-                                                int64_t l, int64_t Bp, int N, double n0, double n1, double n2,
-                                                double n3) {
+                                                double gamma0, int64_t l, int64_t Bp, int N, double n0, double n1,
+                                                double n2, double n3) {
     const int T = N - 1;
     const double G00 = w.G00, iG00 = w.iG00;
-    // lane byte offsets: 2-row wave-blocked pairs (K1, x), 1-row pairs (cs), planes (u)
-    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    // lane byte offsets: 2-row wave-blocked pairs (K1, x), planes (cs, u)
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const double dg = gamma - gamma0;                     // SIG: step size relative to the first trial's
     const char* Kb = reinterpret_cast<const char*>(K1);   // stage stride 2 rows
-    const char* Cb = reinterpret_cast<const char*>(cs);   // stage stride 1 row
+    const char* Cb = reinterpret_cast<const char*>(cs);   // stage stride 2 planes = 1 row
     const char* Ub = reinterpret_cast<const char*>(u);    // stage stride 2 planes = 1 row
     const char* Xb = reinterpret_cast<const char*>(xn);   // stage stride 2 rows
     const char* Ob = reinterpret_cast<const char*>(un);   // stage stride 1 row
@@ -254,24 +261,26 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         q.k0 = bld2<CP>(rK, o2, 0);
         q.k1 = bld2<CP>(rK, o2, WROW);
-        q.c = bld2<CP>(rsrc(Cb + (int64_t)t * row), o2c, 0);
+        const auto rC = rsrc(Cb + (int64_t)t * row);
+        q.cg = bld1<CP>(rC, o1, 0);
+        q.s1 = SIG ? bld1<CP>(rC, o1, plane) : 0.0;
         q.u0 = U0Z ? 0.0 : bld1<CP>(rsrc(Ub + (int64_t)t * row), o1, 0);
     };
     const gym::PolyRegs pk = gym::poly_vgprs();   // loop-invariant coefficients held in VGPRs
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
     fetch(pre, 0);
-    pin(pre.k0); pin(pre.k1); pin(pre.c); pin(pre.u0);
+    pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
     prio_start<1>();
     for (int t = 0; t < T; ++t) {
         prio_band<1>(t, T);
-        const double2 k0 = pre.k0, k1 = pre.k1, c = pre.c;
-        const double u0 = pre.u0;
+        const double2 k0 = pre.k0, k1 = pre.k1;
+        const double cg = pre.cg, s1 = pre.s1, u0 = pre.u0;
         if (t + 1 < T) fetch(pre, t + 1);
         const double* urt = ur + 2 * t;
         const double s0 = -(G00 * (u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
         const double v0 = u0 + gamma * s0;                 // U0Z: u0 = ur0 = 0  =>  v0 = +0 exactly
         const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
-        const double v1 = (c.x + kx) + gamma * c.y;
+        const double v1 = SIG ? __builtin_fma(dg, s1, cg + kx) : cg + kx;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
         J += xcost(ka.w.Q, n0, n1, n2, n3, xr + 4 * t);
@@ -421,18 +430,38 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const d
     smax_out = S.smax;
 }
 
-// Solver sweep of one lane: writes K row 1 and (c1 = u1 - K1 x, sigma1), prefetching stage t-1's
-// streams while stage t computes.  U0Z: the tau1 channel is identically zero (u0 = ur0 = 0,
-// GYM_FLAG_U0_ZERO) and its plane is not read.
-template <bool U0Z>
+// What a solver sweep stores: K row 1 + cg (every iteration), sigma1 only (re-run for the trials 2..20 and
+// the final sigma), or all three (gamma sweeps).
+enum SweepOut { OUT_SOLVER = 0, OUT_SIGMA = 1, OUT_ALL = 2 };
+
+// stage t's sweep outputs: K row 1 (wave-blocked pairs), cg (plane 0 of cs), sigma1 (plane 1)
+template <int OUT>
+__device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int t, uint32_t row, uint32_t plane,
+                                            uint32_t o2, uint32_t o1, double2 xa, double2 xb, double ut1, double g0,
+                                            double k0, double k1, double k2, double k3, double s1) {
+    const auto rC = rsrc(Cb + (int64_t)t * row);
+    if (OUT != OUT_SIGMA) {
+        const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        bst2(rK, o2, 0, k0, k1);
+        bst2(rK, o2, WROW, k2, k3);
+        bst1(rC, o1, 0, __builtin_fma(g0, s1, c1));
+    }
+    if (OUT != OUT_SOLVER) bst1(rC, o1, plane, s1);
+}
+
+// Solver sweep of one lane: writes K row 1 and cg = (u1 - K1 x) + gamma0 sigma1 (and / or sigma1, OUT),
+// prefetching stage t-1's streams while stage t computes.  U0Z: the tau1 channel is identically zero
+// (u0 = ur0 = 0, GYM_FLAG_U0_ZERO) and its plane is not read.
+template <bool U0Z, int OUT>
 __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
                                                      const double2* __restrict__ x, const double* __restrict__ u,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
-                                                     double2* __restrict__ K1, double2* __restrict__ cs, int64_t l,
-                                                     int64_t Bp, int N, double& dJ_out, double& smax_out) {
+                                                     double2* __restrict__ K1, double* __restrict__ cs, double g0,
+                                                     int64_t l, int64_t Bp, int N, double& dJ_out, double& smax_out) {
     const int T = N - 1;
-    // lane byte offsets: 2-row wave-blocked pairs (x, K1), 1-row pairs (cs), planes (u)
-    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    // lane byte offsets: 2-row wave-blocked pairs (x, K1), planes (cs, u)
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Xb = reinterpret_cast<const char*>(x);    // stage stride 2 rows
     const char* Ub = reinterpret_cast<const char*>(u);    // stage stride 1 row
@@ -464,11 +493,7 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         double k0, k1, k2, k3, s0, s1;
         const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
         S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
-        const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
-        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        bst2(rK, o2, 0, k0, k1);
-        bst2(rK, o2, WROW, k2, k3);
-        bst2(rsrc(Cb + (int64_t)t * row), o2c, 0, c1, s1);
+        store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, xa, xb, ut1, g0, k0, k1, k2, k3, s1);
     }
     dJ_out = S.dJ;
     smax_out = S.smax;
@@ -487,15 +512,15 @@ struct CkBlock {
     double u0[CKI], u1[CKI];
 };
 
-template <bool U0Z>
+template <bool U0Z, int OUT>
 __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& w,
                                                         const double2* __restrict__ x, const double* __restrict__ u,
                                                         const double* __restrict__ xr, const double* __restrict__ ur,
-                                                        double2* __restrict__ K1, double2* __restrict__ cs,
+                                                        double2* __restrict__ K1, double* __restrict__ cs, double g0,
                                                         double2* __restrict__ lds, int64_t l, int64_t Bp, int N,
                                                         double& dJ_out, double& smax_out) {
     const int T = N - 1;
-    const uint32_t o2 = wbo(l, 2), o2c = (uint32_t)l * 16u, o1 = (uint32_t)l * 8u;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Xb = reinterpret_cast<const char*>(x);
     const char* Ub = reinterpret_cast<const char*>(u);
@@ -563,11 +588,7 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
                 double k0, k1, k2, k3, s0, s1;
                 const KArgs ka = kernarg_consts();
                 S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
-                const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
-                const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-                bst2(rK, o2, 0, k0, k1);
-                bst2(rK, o2, WROW, k2, k3);
-                bst2(rsrc(Cb + (int64_t)t * row), o2c, 0, c1, s1);
+                store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, xa, xb, ut1, g0, k0, k1, k2, k3, s1);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -974,38 +995,42 @@ struct Range {
     int64_t lo, hi;
 };
 
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, int OUT = OUT_SOLVER>
 __device__ __forceinline__ void backward_solver(const Dyn& m, const KW& w, const double2* __restrict__ x,
                                                 const double* __restrict__ u, const double* __restrict__ xr,
                                                 const double* __restrict__ ur, double2* __restrict__ K1,
-                                                double2* __restrict__ cs, double* __restrict__ dJ,
+                                                double* __restrict__ cs, double g0, double* __restrict__ dJ,
                                                 double* __restrict__ smax, double* __restrict__ hist_smax, int64_t l,
                                                 int64_t Bp, int N, int k, int hist_len, double2* __restrict__ lds) {
     double d, s;
     if (CK)
-        backward_solver_lane_ck<U0Z>(m, w, x, u, xr, ur, K1, cs, lds, l, Bp, N, d, s);
+        backward_solver_lane_ck<U0Z, OUT>(m, w, x, u, xr, ur, K1, cs, g0, lds, l, Bp, N, d, s);
     else
-        backward_solver_lane<U0Z>(m, w, x, u, xr, ur, K1, cs, l, Bp, N, d, s);
+        backward_solver_lane<U0Z, OUT>(m, w, x, u, xr, ur, K1, cs, g0, l, Bp, N, d, s);
+    if (OUT == OUT_SIGMA) return;   // a re-run: the lane's dJ / smax are those of the original sweep
     dJ[l] = d;
     smax[l] = s;
     if (hist_smax && k < hist_len) hist_smax[(int64_t)k * Bp + l] = s;
 }
 
+#define GYM_NT_BACKWARD_PARAMS                                                                                  \
+    Dyn m, KW w, const double2 *__restrict__ x, const double *__restrict__ u, const double *__restrict__ xr,   \
+        const double *__restrict__ ur, double2 *__restrict__ K1, double *__restrict__ cs, double g0,           \
+        double *__restrict__ dJ, double *__restrict__ smax, const int32_t *__restrict__ status,               \
+        double *__restrict__ hist_smax, Range rg, int64_t Bp, int N, int k, int hist_len
+#define GYM_NT_BACKWARD_BODY(OUT)                                                                               \
+    GYM_TRACE_WAVE(0);                                                                                          \
+    const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;                                          \
+    GYM_CK_LDS(CK, U0Z);                                                                                        \
+    if (l >= rg.hi || status[l] != GYM_ACTIVE) return;                                                          \
+    backward_solver<U0Z, CK, OUT>(m, w, x, u, xr, ur, K1, cs, g0, dJ, smax, hist_smax, l, Bp, N, k, hist_len, ck_lds);
+
+// the solver's serial-schedule sweep (K1, cg) ...
 template <bool U0Z, bool CK>
-__global__ __launch_bounds__(BLK, 4) void k_nt_backward(Dyn m, KW w, const double2* __restrict__ x,
-                                                        const double* __restrict__ u, const double* __restrict__ xr,
-                                                        const double* __restrict__ ur, double2* __restrict__ K1,
-                                                        double2* __restrict__ cs, double* __restrict__ dJ,
-                                                        double* __restrict__ smax,
-                                                        const int32_t* __restrict__ status,
-                                                        double* __restrict__ hist_smax, Range rg, int64_t Bp, int N,
-                                                        int k, int hist_len) {
-    GYM_TRACE_WAVE(0);
-    const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
-    GYM_CK_LDS(CK, U0Z);
-    if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
-    backward_solver<U0Z, CK>(m, w, x, u, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, k, hist_len, ck_lds);
-}
+__global__ __launch_bounds__(BLK, 4) void k_nt_backward(GYM_NT_BACKWARD_PARAMS) { GYM_NT_BACKWARD_BODY(OUT_SOLVER) }
+// ... and the same sweep also storing sigma1, for the gamma sweeps of gym_newton_gamma_sweep
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK, 4) void k_nt_backward_all(GYM_NT_BACKWARD_PARAMS) { GYM_NT_BACKWARD_BODY(OUT_ALL) }
 
 struct SolverCtl {
     double tol, beta, c, gamma0;
@@ -1040,7 +1065,7 @@ struct TrialIO {
 // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass).
 template <bool U0Z, bool CK>
 __device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const SolverCtl& a, const TrialIO& io,
-                                             const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                             const double2* __restrict__ K1, const double* __restrict__ cs,
                                              const double* __restrict__ xr, const double* __restrict__ ur,
                                              double* __restrict__ cost, const double* __restrict__ dJ,
                                              const double* __restrict__ smax, double* __restrict__ gamma,
@@ -1050,8 +1075,8 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const So
                                              double* __restrict__ hist_cost, int64_t l, int64_t Bp, int N) {
     const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
     const double g = a.gamma0;
-    const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
-                                                   xa.y, xb.x, xb.y);
+    const double Jn = rollout_cform<true, U0Z, false, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, g, l, Bp, N,
+                                                          xa.x, xa.y, xb.x, xb.y);
     n_roll[l] += 1;
     if (Jn < cost[l] + a.c * g * dJ[l]) {  // strict Armijo test (:361)
         n_iter[l] += 1;
@@ -1066,7 +1091,7 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const So
 
 template <bool U0Z, bool CK>
 __global__ __launch_bounds__(BLK, 4) void k_nt_trial(Dyn m, KW w, SolverCtl a, TrialIO io,
-                                                     const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                     const double2* __restrict__ K1, const double* __restrict__ cs,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
                                                      double* __restrict__ cost, const double* __restrict__ dJ,
                                                      const double* __restrict__ smax, double* __restrict__ gamma,
@@ -1089,7 +1114,7 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(Dyn m, KW w, SolverCtl a, T
                                                      const double2* __restrict__ xb_in,
                                                      const double* __restrict__ ub_in, int kb, int nb_b,
                                                      Range rb, Range rt, double2* __restrict__ K1,
-                                                     double2* __restrict__ cs, const double* __restrict__ xr,
+                                                     double* __restrict__ cs, const double* __restrict__ xr,
                                                      const double* __restrict__ ur, double* __restrict__ cost,
                                                      double* __restrict__ dJ, double* __restrict__ smax,
                                                      double* __restrict__ gamma, int32_t* __restrict__ status,
@@ -1101,8 +1126,8 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(Dyn m, KW w, SolverCtl a, T
     if ((int)blockIdx.x < nb_b) {
         const int64_t l = rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
         if (l >= rb.hi || status[l] != GYM_ACTIVE) return;
-        backward_solver<U0Z, CK>(m, w, xb_in, ub_in, xr, ur, K1, cs, dJ, smax, hist_smax, l, Bp, N, kb, a.hist_len,
-                                 ck_lds);
+        backward_solver<U0Z, CK>(m, w, xb_in, ub_in, xr, ur, K1, cs, a.gamma0, dJ, smax, hist_smax, l, Bp, N, kb,
+                                 a.hist_len, ck_lds);
     } else {
         const int64_t l = rt.lo + (int64_t)(blockIdx.x - nb_b) * BLK + threadIdx.x;
         if (l >= rt.hi || status[l] != GYM_ACTIVE) return;
@@ -1114,7 +1139,7 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(Dyn m, KW w, SolverCtl a, T
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
 template <bool U0Z>
 __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a, TrialIO io,
-                                                       const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                       const double2* __restrict__ K1, const double* __restrict__ cs,
                                                        const double* __restrict__ xr, const double* __restrict__ ur,
                                                        const double* __restrict__ cost, const double* __restrict__ dJ,
                                                        const int32_t* __restrict__ retry_list,
@@ -1129,8 +1154,8 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a,
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
         const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
-        const double Jn = rollout_cform<false, U0Z>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, l, Bp, N, xa.x,
-                                                    xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<false, U0Z, true>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, a.gamma0, l,
+                                                          Bp, N, xa.x, xa.y, xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
     }
 }
@@ -1138,7 +1163,7 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a,
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
 template <bool U0Z, bool CK>
 __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, TrialIO io,
-                                                  const double2* __restrict__ K1, const double2* __restrict__ cs,
+                                                  const double2* __restrict__ K1, const double* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
                                                   double* __restrict__ cost, const double* __restrict__ smax,
                                                   double* __restrict__ gamma, int32_t* __restrict__ status,
@@ -1164,8 +1189,8 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
         const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
-        const double Jn = rollout_cform<true, U0Z, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, l, Bp, N, xa.x,
-                                                       xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<true, U0Z, true, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, a.gamma0, l,
+                                                             Bp, N, xa.x, xa.y, xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -1209,7 +1234,7 @@ __global__ __launch_bounds__(BLK) void k_gamma_sweep(Dyn m, KW w, const double2*
 template <bool U0Z>
 __global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const double2* __restrict__ x,
                                                         const double* __restrict__ u, const double2* __restrict__ K1,
-                                                        const double2* __restrict__ cs,
+                                                        const double* __restrict__ cs, double g0,
                                                         const double* __restrict__ gammas, int G,
                                                         const double* __restrict__ xr, const double* __restrict__ ur,
                                                         const int32_t* __restrict__ status,
@@ -1223,8 +1248,9 @@ __global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const doubl
         return;
     }
     const double2 a = x[wix(0, 0, 2, l, Bp)], b = x[wix(0, 1, 2, l, Bp)];
-    cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, false, 0>(m, w, u, K1, cs, xr, ur, nullptr, nullptr,
-                                                                        gammas[g], l, Bp, N, a.x, a.y, b.x, b.y);
+    cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, true, false, 0>(m, w, u, K1, cs, xr, ur, nullptr,
+                                                                              nullptr, gammas[g], g0, l, Bp, N, a.x,
+                                                                              a.y, b.x, b.y);
 }
 
 // Deterministic two-stage statistics reduction (fixed lane->thread map, fixed trees).
@@ -1291,6 +1317,30 @@ __global__ __launch_bounds__(64 * NSTAT) void k_stats_final(const double* __rest
     if (threadIdx.x == 0) *counter = 0;  // the retry list is rebuilt every iteration
 }
 
+// sigma1 re-run: the sweep of an earlier pass, recomputed (same inputs, same code: the same bits) into the
+// sigma1 plane.  retry mode (list != nullptr): the lanes list[0 .. *count) at the iterate (x, u); final mode:
+// the lanes whose last iteration started from this buffer, (n_iter - 1) & 1 == parity (one launch per
+// buffer, so the streams' base addresses stay wave-uniform).
+template <bool U0Z, bool CK>
+__global__ __launch_bounds__(BLK, 4) void k_nt_sigma(Dyn m, KW w, const double2* __restrict__ x,
+                                                     const double* __restrict__ u, const double* __restrict__ xr,
+                                                     const double* __restrict__ ur, double* __restrict__ cs,
+                                                     const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                                     const int32_t* __restrict__ n_iter, int parity, int64_t B,
+                                                     int64_t Bp, int N) {
+    GYM_CK_LDS(CK, U0Z);
+    const int64_t n = list ? (int64_t)*count : B;
+    for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
+        const int64_t l = list ? (int64_t)list[i] : i;
+        if (!list) {
+            const int it = n_iter[l];
+            if (it <= 0 || ((it - 1) & 1) != parity) continue;
+        }
+        backward_solver<U0Z, CK, OUT_SIGMA>(m, w, x, u, xr, ur, nullptr, cs, 0.0, nullptr, nullptr, nullptr, l, Bp, N,
+                                            0, 0, ck_lds);
+    }
+}
+
 __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restrict__ res_buf, int64_t B, int k_done) {
     const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= B) return;
@@ -1300,9 +1350,10 @@ __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restr
     }
 }
 
-// sigma of each lane's last iteration, lane-major (B,T,2): sigma1 from the sweep's (c1, sigma1) stream,
-// sigma0 = -(2R0 (u0 - ur0)) / (2R0) recomputed from that iteration's controls, buffer (n_iter-1) & 1.
-__global__ void k_finalize_sigma(KW w, const double2* __restrict__ cs, const double* __restrict__ u0b,
+// sigma of each lane's last iteration, lane-major (B,T,2): sigma1 from the sigma1 plane (k_nt_sigma re-ran the
+// lane's last sweep into it), sigma0 = -(2R0 (u0 - ur0)) / (2R0) recomputed from that iteration's controls,
+// buffer (n_iter-1) & 1.
+__global__ void k_finalize_sigma(KW w, const double* __restrict__ cs, const double* __restrict__ u0b,
                                  const double* __restrict__ u1b, const double* __restrict__ ur,
                                  const int32_t* __restrict__ n_iter, double* __restrict__ sig, int64_t B, int64_t Bp,
                                  int T) {
@@ -1315,7 +1366,7 @@ __global__ void k_finalize_sigma(KW w, const double2* __restrict__ cs, const dou
     if (it > 0) {
         const double* u = ((it - 1) & 1) ? u1b : u0b;
         s0 = -(w.G00 * (u[pix(t, 0, 2, lane, Bp)] - ur[2 * t])) * w.iG00;
-        s1 = cs[(int64_t)t * Bp + lane].y;
+        s1 = cs[pix(t, 1, 2, lane, Bp)];
     }
     sig[2 * o] = s0;
     sig[2 * o + 1] = s1;
@@ -1539,9 +1590,15 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
                               const double* other, double* total, hipStream_t st) {
     const int64_t n = rg.hi - rg.lo;
     const double2* K1 = (const double2*)b->K1;
-    const double2* cs = (const double2*)b->cs;
+    const double* cs = b->cs;
     double* hc = a->record_history ? b->hist_cost : nullptr;
     if (a->max_ls > 1 && n > 0) {
+        {   // the lanes that reject trial 1 need sigma1: re-run their sweep of this iteration into its plane
+            TimedLaunch tl(b->timing, 7, st);
+            hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m),
+                               kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
+                               (const int32_t*)nullptr, -1, b->B, b->Bp, b->N);
+        }
         {
             TimedLaunch tl(b->timing, 2, st);
             const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
@@ -1579,14 +1636,14 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     {
         TimedLaunch tl(b->timing, 0, st);
         hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
-                           (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
+                           (double2*)b->K1, b->cs, a->gamma0, b->dJ, b->smax, b->status,
                            hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     {
         TimedLaunch tl(b->timing, 1, st);
         hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, (const double2*)b->K1,
-                           (const double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
+                           (const double*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
                            all, b->Bp, b->N);
     }
@@ -1623,7 +1680,7 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
         TimedLaunch tl(b->timing, (p & 1) ? 5 : 6, st);
         hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io,
                            (const double2*)b->x[kb & 1], b->u[kb & 1], kb, nb_b, rb, rt, (double2*)b->K1,
-                           (double2*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
+                           b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters + ht,
                            hist ? b->hist_cost : nullptr, hist ? b->hist_smax : nullptr, b->Bp, b->N);
     }
@@ -1654,15 +1711,23 @@ int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batc
     if (x_out && (e = gym_unpack_lanes(b->x[0], b->x[1], b->res_buf, x_out, b->B, b->Bp, b->N, 4, 2, s))) return e;
     if (u_out && (e = gym_unpack_lanes(b->u[0], b->u[1], b->res_buf, u_out, b->B, b->Bp, T, 2, 1, s))) return e;
     if (K_out && (e = gym_unpack_gains(b->K1, K_out, b->B, b->Bp, T, s))) return e;
-    if (sig_out && (e = gym_newton_sigma(w, b, sig_out, s))) return e;
+    if (sig_out && (e = gym_newton_sigma(m, w, b, sig_out, s))) return e;
     return 0;
 }
 
-int gym_newton_sigma(const gym_weights* w, const gym_batch* b, double* sig_out, void* s) {
-    if (!w || bad_batch(b) || !sig_out) return GYM_EINVAL;
+int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* b, double* sig_out, void* s) {
+    if (!m || !w || bad_batch(b) || !sig_out) return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
     const int T = b->N - 1;
-    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, (hipStream_t)s, kw(*w),
-                       (const double2*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
+    for (int parity = 0; parity < 2; ++parity) {   // sigma1 of each lane's last sweep, one launch per buffer
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_sigma), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+                           (const double2*)b->x[parity], b->u[parity], b->x_ref, b->u_ref, b->cs,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr, b->n_iter, parity, b->B, b->Bp, b->N);
+        const int e = launch_status();
+        if (e) return e;
+    }
+    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, st, kw(*w),
+                       (const double*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
     return launch_status();
 }
 
@@ -1682,21 +1747,21 @@ int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, c
     return launch_status();
 }
 
-int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_batch* b, int32_t k,
-                           const double* gammas, int32_t G, double* cost_out, void* s) {
-    if (!m || !w || bad_batch(b) || k < 0 || !gammas || !cost_out || G < 1 ||
+int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
+                           int32_t k, const double* gammas, int32_t G, double* cost_out, void* s) {
+    if (!m || !w || !a || bad_batch(b) || k < 0 || !gammas || !cost_out || G < 1 ||
         (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8)
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const TrialIO io = trial_io(b, k);
-    // iteration k's backward sweep (K1, cs, dJ, smax: the values iteration k itself computes)
-    hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
-                       io.x, io.u, b->x_ref, b->u_ref, (double2*)b->K1, (double2*)b->cs, b->dJ, b->smax, b->status,
+    // iteration k's backward sweep (K1, cg, dJ, smax: the values iteration k itself computes) plus sigma1
+    hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward_all), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+                       io.x, io.u, b->x_ref, b->u_ref, (double2*)b->K1, b->cs, a->gamma0, b->dJ, b->smax, b->status,
                        (double*)nullptr, Range{0, b->B}, b->Bp, b->N, (int)k, 0);
     int e = launch_status();
     if (e) return e;
     hipLaunchKernelGGL(U0Z_SEL(b, k_nt_gamma_sweep), dim3(sweep_grid(b->Bp, G)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
-                       io.x, io.u, (const double2*)b->K1, (const double2*)b->cs, gammas, (int)G, b->x_ref, b->u_ref,
+                       io.x, io.u, (const double2*)b->K1, (const double*)b->cs, a->gamma0, gammas, (int)G, b->x_ref, b->u_ref,
                        b->status, cost_out, b->B, b->Bp, b->N);
     return launch_status();
 }

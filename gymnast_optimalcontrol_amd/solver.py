@@ -61,7 +61,16 @@ class SolveResult:
 class BatchedNewtonSolver:
     """Owns the device buffers of a batch of ``B`` lanes that share x_ref / u_ref."""
 
-    PIPELINE_MIN_LANES = 8192
+    # The pipelined schedule pays off once the batch is more than ~1.25 wavefronts per SIMD (measured on one
+    # MI355X, profiles/r01_batch_sweep.log: serial is ahead up to 65,536 lanes = 1 wave/SIMD, pipelined from
+    # 98,304 on; below that the solve is latency-bound and the two phases per iteration cost more than they
+    # overlap).  In units of lanes per compute unit (4 SIMDs x 64 lanes x 1.25).
+    PIPELINE_MIN_LANES_PER_CU = 320
+
+    @staticmethod
+    def pipeline_min_lanes(device) -> int:
+        n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+        return BatchedNewtonSolver.PIPELINE_MIN_LANES_PER_CU * n_cu
 
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
@@ -83,7 +92,7 @@ class BatchedNewtonSolver:
         self.x = [e(N, 2, Bp, 2), e(N, 2, Bp, 2)]
         self.u = [e(T, 2, Bp, 1), e(T, 2, Bp, 1)]      # control planes (tau1, tau2)
         self.K1 = e(T, 2, Bp, 2)                       # gain row 1, pairs
-        self.cs = e(T, 1, Bp, 2)                       # (c1 = u1 - K1 x, sigma1), pairs
+        self.cs = e(T, 2, Bp, 1)                       # planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1
         self.cost, self.dJ, self.smax, self.gamma = e(Bp), e(Bp), e(Bp), e(Bp)
         i32 = torch.int32
         self.status, self.n_iter, self.res_buf, self.n_roll = (e(Bp, dt=i32) for _ in range(4))
@@ -92,7 +101,7 @@ class BatchedNewtonSolver:
         self.cand_ok = torch.zeros((max(int(max_ls), 1), Bp), dtype=torch.uint8, device=dev)
         self.partials = e(256 * 8)
         self.stats = torch.zeros(24, dtype=F64, device=dev)     # [0,8) totals, [8,16) / [16,24) halves
-        self.pipeline = (self.B >= self.PIPELINE_MIN_LANES) if pipeline is None else bool(pipeline)
+        self.pipeline = (self.B >= self.pipeline_min_lanes(dev)) if pipeline is None else bool(pipeline)
         self.max_iters = None
         self.hist_len = int(hist_len)
         self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
@@ -218,7 +227,7 @@ class BatchedNewtonSolver:
             raise ValueError("gamma_sweep needs at least one step size")
         J = torch.empty((G, self.Bp), dtype=F64, device=self.eng.device)
         _lib.check(self.eng.lib.gym_newton_gamma_sweep(C.byref(self.eng.model), C.byref(self.eng._w),
-                                                       C.byref(self.batch), self.k, g.data_ptr(), G, J.data_ptr(),
+                                                       C.byref(self.armijo), C.byref(self.batch), self.k, g.data_ptr(), G, J.data_ptr(),
                                                        self.eng.stream), "gym_newton_gamma_sweep")
         return J[:, :self.B].t()
 
@@ -234,9 +243,10 @@ class BatchedNewtonSolver:
         return self.eng.unpack(self.u[buf], self.B)
 
     def sigma(self) -> torch.Tensor:
-        """sigma (B,T,2) of every lane's most recent backward sweep."""
+        """sigma (B,T,2) of every lane's last completed iteration (its sweep re-run: sigma1 is not streamed)."""
         s = torch.empty((self.B, self.T, 2), dtype=F64, device=self.eng.device)
-        _lib.check(self.eng.lib.gym_newton_sigma(C.byref(self.eng._w), C.byref(self.batch), s.data_ptr(),
+        _lib.check(self.eng.lib.gym_newton_sigma(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.batch),
+                                                 s.data_ptr(),
                                                  self.eng.stream), "gym_newton_sigma")
         return s
 

@@ -91,9 +91,9 @@ typedef struct gym_armijo {
 
 /* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
  * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
- * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p).  A pair is recorded only if the
- * previous one of its kind was collected. */
-#define GYM_NK 7
+ * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p), 7 sigma1 re-run of the lanes that
+ * backtrack.  A pair is recorded only if the previous one of its kind was collected. */
+#define GYM_NK 8
 typedef struct gym_timing {
     void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
     double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
@@ -110,7 +110,7 @@ typedef struct gym_batch {
     double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered (wave-blocked) */
     double* u[2];       /* (T,2,Bp) control planes, double-buffered               */
     double* K1;         /* (T,2,Bp) double2 feedback gains, row 1 (wave-blocked)  */
-    double* cs;         /* (T,Bp)   double2 (c1 = u1 - K1 x, sigma1) of the sweep  */
+    double* cs;         /* (T,2,Bp) planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1 (re-run only) */
     const double* x_ref;/* (N,4) shared reference states                          */
     const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
     double* cost;       /* (Bp) current J_k                                       */
@@ -222,8 +222,9 @@ int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batc
  * res_buf) from its checkpoints and the controls u[buf]: x_{t+1} = RK4(x_t, u_t) from each checkpoint, the
  * trial's arithmetic bit for bit.  Lanes [0, B); a no-op without the flag. */
 int gym_newton_fill_states(const gym_model* m, const gym_batch* bt, int32_t buf, void* stream);
-/* sigma (B,T,2) of each lane's most recent backward sweep (sigma1 from cs, sigma0 recomputed). */
-int gym_newton_sigma(const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);
+/* sigma (B,T,2) of each lane's last completed iteration (n_iter - 1): sigma1 by re-running that iteration's
+ * sweep (the solver does not stream sigma1; the re-run reproduces it bit for bit), sigma0 recomputed. */
+int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);
 
 /* ---------------- Armijo gamma sweeps (plot_armijo_line_search, trajectory_generation.py:254-296) ---------------- */
 /* J(gamma_g) = total_cost (:231-252) of forward_closed_loop_update(x, u, K, sigma, gamma_g) (:218-229) for G step
@@ -234,11 +235,11 @@ int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, c
                     const double* sigma, const double* gammas, int32_t G, const double* x_ref, const double* u_ref,
                     double* cost_out, int64_t B, int64_t Bp, int32_t N, void* stream);
 /* The same curve for every lane of a batched solve at the iterate iteration k starts from (k = iterations done;
- * either schedule): runs iteration k's backward sweep (K1, cs, dJ, smax -- exactly what iteration k computes, so
+ * either schedule): runs iteration k's backward sweep (K1, cg, dJ, smax -- exactly what iteration k computes, so
  * the solve is unaffected) and then the Armijo trial's own rollout for each gamma_g: at the trial's step sizes
  * gamma0 beta^i the costs equal the trial costs bit for bit.  cost_out (G,Bp); NaN for lanes not ACTIVE. */
-int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_batch* bt, int32_t k,
-                           const double* gammas, int32_t G, double* cost_out, void* stream);
+int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt,
+                           int32_t k, const double* gammas, int32_t G, double* cost_out, void* stream);
 
 /* ---------------- LQR / receding-horizon MPC trackers (trajectory_tracking.py) ---------------- */
 /* Time-varying LQR gains over windows of a stage array.  Stages: A (S,4,4), B (S,4,2) [device], continuous
