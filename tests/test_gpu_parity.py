@@ -247,6 +247,44 @@ def test_ragged_batches_and_padding(B, task2_refs):
     assert last[1] == pytest.approx(o["cost"].sum(), rel=1e-10)
 
 
+@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("max_iters", [12, 120])
+def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, pipeline, max_iters):
+    """K and sigma of each lane's last iteration (newton_Algorithm's return values) after backtracking, LS
+    failures, a NaN lane and the max_iters cut-off.  sigma1 is not streamed by the solver: gym_newton_sigma
+    re-runs each lane's last sweep from the state buffer that iteration started from, and the lanes that
+    backtrack re-run theirs inside the iteration; both must reproduce the oracle's values."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from oracle import c_oracle
+    xr, ur, _ = task2_refs
+    B = 160
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
+    x0[:20, 2:] = np.random.default_rng(6).uniform(-2.0, 2.0, (20, 2))      # seed-14-like lanes: early LS failures
+    x0[9] = np.nan
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=1.0, pipeline=pipeline).solve(x0, max_iters)
+    o = c_oracle.newton_solve(x0, xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=1.0)
+    ni, st = r.n_iter.cpu().numpy(), r.status.cpu().numpy()
+    same = (ni == o["n_iter"]) & (st == o["status"]) & (r.n_rollouts.cpu().numpy() == o["n_rollouts"])
+    assert same.mean() >= 0.97, f"decisions differ on {np.flatnonzero(~same)}"
+    assert st[9] == _lib.LS_FAILED and np.isnan(r.sigma.cpu().numpy()[9]).any()
+    assert (r.n_rollouts.cpu().numpy() > ni).any()                           # some lanes backtracked
+    if max_iters == 120:
+        assert (st == _lib.LS_FAILED).sum() >= 2
+    ok = same & np.isfinite(o["cost"])
+    # Far from convergence (gamma_0 = 1, wide starts) Newton iterates amplify rounding-level differences from
+    # iteration to iteration, so after 120 iterations the two implementations' iterates differ by ~1e-5
+    # relative; a sigma taken from the wrong iterate (the other state buffer) would differ by O(1).
+    tol = 1e-8 if max_iters <= 12 else 1e-3
+    for name, ref in (("sigma", o["sigma"]), ("K", o["K"]), ("x", o["x"]), ("u", o["u"])):
+        got = getattr(r, name).cpu().numpy()[ok]
+        assert rel_l2(got, ref[ok]) < tol, name
+        lane_err = np.linalg.norm((got - ref[ok]).reshape(ok.sum(), -1), axis=1) / \
+            np.maximum(np.linalg.norm(ref[ok].reshape(ok.sum(), -1), axis=1), 1e-300)
+        assert lane_err.max() < 10 * tol, (name, int(np.argmax(lane_err)))
+
+
 def test_single_trial_line_search_and_nan_lane(task2_refs):
     """max_ls = 1 (no retry path) and a NaN initial state (NaN costs compare false -> LS failure)."""
     from gymnast_optimalcontrol_amd import _lib
