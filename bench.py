@@ -166,8 +166,10 @@ def main():
     ap.add_argument("--workload", choices=("newton", "mpc"), default="newton",
                     help="newton: the north-star metric (cfg 3); mpc: BASELINE cfg 5")
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
-    ap.add_argument("--schedule", choices=("auto", "serial", "pipelined"), default="auto",
+    ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
                     help="solver schedule (auto: the solver's choice for the batch size)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="persistent schedule: iterations per launch (0: all of max_iters in one launch)")
     a = ap.parse_args()
     if a.batch is None:
         a.batch = 8192 if a.workload == "mpc" else 262144
@@ -191,7 +193,8 @@ def main():
     lo, hi = gd.shard_range(total, rank, world)
     eng = AcrobotEngine()
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20,
-                                 pipeline={"auto": None, "serial": False, "pipelined": True}[a.schedule])
+                                 pipeline={"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule],
+                                 persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk)
     if not a.no_timing:
         solver.enable_timing()
     x0_dev = eng.t(x0_all[lo:hi])                  # inputs resident in HBM before the timed region
@@ -245,7 +248,14 @@ def main():
         for kind, (ms, launches) in kt.items():
             if launches:
                 kern[kind] = {"avg_ms": ms / launches, "launches": launches}
-        if "phase_odd" in kern:
+        if "run" in kern:
+            # persistent schedule: every lane-iteration (sweep + trial) runs inside the run launches
+            dom = "run"
+            per_launch = lane_its * ab["iteration"] / kern["run"]["launches"]
+            kern["run"]["algorithmic_bytes_per_launch"] = per_launch
+            kern["run"]["achieved_GBs"] = per_launch / (kern["run"]["avg_ms"] * 1e-3) / 1e9
+            bytes_per_lane, unit_note = ab["iteration"], "sweep + trial of one lane-iteration"
+        elif "phase_odd" in kern:
             # pipelined schedule: every lane-iteration = one sweep + one trial, all inside the phase launches
             # (2 * iterations + 1 per solve; a launch's time is recorded whenever its timing slot is free)
             dom = "phase"
@@ -283,7 +293,7 @@ def main():
                            "survey_bytes_per_iteration": ab["survey_per_iteration"],
                            "whole_solve_GBs_at_survey_bytes": value * ab["survey_per_iteration"] / 1e9 / world}
         out["kernels"] = kern
-        out["schedule"] = "pipelined" if solver.pipeline else "serial"
+        out["schedule"] = "persistent" if solver.persistent else ("pipelined" if solver.pipeline else "serial")
     if parity is not None:
         out["parity"] = parity
     if rank == 0 and world == 1 and not a.no_cpu:

@@ -20,6 +20,7 @@
 // primitives it calls) and dynamics.py.  See include/gymnast_acrobot.h for the ABI.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "acrobot_device.hpp"
@@ -135,12 +136,31 @@ __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 // / 2.49 ms of a 2.5 ms launch), so the launch ends with one wave per SIMD and few loads in flight.  With
 // the bands the lagging waves win arbitration, all finish together, and the launch is 6% shorter.
 // The stage index is wave-uniform: these are scalar compares and s_setprio, no VALU.
-// KIND: 0 = sweep, 1 = trial.  (Measured alternatives: sweep banded above the trial, 1.3% slower; trial above
-// the sweep, 9.6% slower.)
+// KIND: 0 = sweep, 1 = trial, 2 = no banding (the caller sets the priority).  (Measured alternatives: sweep
+// banded above the trial, 1.3% slower; trial above the sweep, 9.6% slower.)
+constexpr int PRIO_NONE = 2;
 template <int KIND>
-__device__ __forceinline__ void prio_start() { __builtin_amdgcn_s_setprio(3); }
+__device__ __forceinline__ void prio_start() {
+    if (KIND != PRIO_NONE) __builtin_amdgcn_s_setprio(3);
+}
+// GYM_PRIO_SHIFT > 0 (measurement variant): cyclic bands of 2^shift stages, priority 3, 2, 1, 0, 3, ...
+#ifndef GYM_PRIO_SHIFT
+#define GYM_PRIO_SHIFT 0
+#endif
 template <int KIND>
 __device__ __forceinline__ void prio_band(int done, int T) {
+    if (KIND == PRIO_NONE) return;
+    if (GYM_PRIO_SHIFT > 0) {
+        if ((done & ((1 << GYM_PRIO_SHIFT) - 1)) == 0) {
+            switch ((done >> GYM_PRIO_SHIFT) & 3) {
+                case 0: __builtin_amdgcn_s_setprio(3); break;
+                case 1: __builtin_amdgcn_s_setprio(2); break;
+                case 2: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+        }
+        return;
+    }
     asm volatile("" : "+s"(T));   // thresholds recomputed per stage (3 SALU) rather than held: no spills
     if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
     else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
@@ -233,7 +253,7 @@ struct TrialStage {
     double u0;           // tau1 control (0 when U0Z)
 };
 
-template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT>
+template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT, bool BAND = true>
 __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const double* __restrict__ u,
                                                 const double2* __restrict__ K1, const double* __restrict__ cs,
                                                 const double* __restrict__ xr, const double* __restrict__ ur,
@@ -270,9 +290,9 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
     fetch(pre, 0);
     pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
-    prio_start<1>();
+    prio_start<BAND ? 1 : PRIO_NONE>();
     for (int t = 0; t < T; ++t) {
-        prio_band<1>(t, T);
+        prio_band<BAND ? 1 : PRIO_NONE>(t, T);
         const double2 k0 = pre.k0, k1 = pre.k1;
         const double cg = pre.cg, s1 = pre.s1, u0 = pre.u0;
         if (t + 1 < T) fetch(pre, t + 1);
@@ -453,7 +473,7 @@ __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int 
 // Solver sweep of one lane: writes K row 1 and cg = (u1 - K1 x) + gamma0 sigma1 (and / or sigma1, OUT),
 // prefetching stage t-1's streams while stage t computes.  U0Z: the tau1 channel is identically zero
 // (u0 = ur0 = 0, GYM_FLAG_U0_ZERO) and its plane is not read.
-template <bool U0Z, int OUT>
+template <bool U0Z, int OUT, bool BAND = true>
 __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
                                                      const double2* __restrict__ x, const double* __restrict__ u,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
@@ -477,9 +497,9 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         if (!U0Z) pu0 = bld1(rU, o1, 0);
     }
     pin(pa); pin(pb); pin(pu0); pin(pu1);
-    prio_start<0>();
+    prio_start<BAND ? 0 : PRIO_NONE>();
     for (int t = T - 1; t >= 0; --t) {
-        prio_band<0>(T - 1 - t, T);
+        prio_band<BAND ? 0 : PRIO_NONE>(T - 1 - t, T);
         const double2 xa = pa, xb = pb;
         const double ut0 = pu0, ut1 = pu1;
         if (t > 0) {
@@ -1196,6 +1216,136 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
 }
 
 // ------------------------------------------------------------------------------------------
+// Persistent schedule (gym_newton_run): every lane runs its own outer iterations k0 .. k1-1 of
+// newton_Algorithm (:329-396) back to back inside ONE launch -- sweep, Armijo trial 1, and only for a lane
+// that rejects it the sigma1 re-run and trials 2..max_ls one after another (:352-365), exactly the
+// sequential search of the reference.  Lanes are independent problems, so nothing orders one lane's
+// iteration against another's: the only dependences are the lane's own stores -> loads through K1 / cs
+// (sweep -> trial) and x / u (trial -> next sweep), ordered by a fence per pass.  The waves of a SIMD drift
+// apart and mix sweep (HBM-heavy) and trial (fp64-heavy) passes by themselves, with no launch boundary, tail
+// or host round trip per iteration.  Per lane the arithmetic is the other schedules' (same device functions):
+// bit-identical results.
+// GYM_RUN_BAND (wave priority): 0 = none (default); 1 = the phase kernels' per-pass progress bands; 2 = cyclic
+// bands of the lane's iteration count.  Same-box A/B (B = 4096 / 32768 / 65536 lanes): 0 and 2 tie, 1 is 4-8%
+// slower (each pass restarting at priority 3 undoes the banding).
+// ------------------------------------------------------------------------------------------
+#ifndef GYM_RUN_BAND
+#define GYM_RUN_BAND 0
+#endif
+// Everything the kernel needs beyond the stage loops' own operands is one by-value struct whose fields are
+// re-read from the kernel-argument segment at each use (run_args(): scalar loads behind an opaque pointer),
+// so that none of its ~20 pointers is held in SGPRs across the stage loops (spilled, they cost v_readlane
+// VALU slots in every stage).  Dyn and KW come first: kernarg_consts() reads them at offsets 0 and 96.
+struct RunArgs {
+    Dyn m;
+    KW w;
+    SolverCtl a;
+    double2* x[2];
+    double* u[2];
+    double2* K1;
+    double* cs;
+    const double* xr;
+    const double* ur;
+    double *cost, *dJ, *smax, *gamma;
+    int32_t *status, *n_iter, *res_buf, *n_roll;
+    double *hist_cost, *hist_smax;
+    int64_t B, Bp;
+    int32_t N, k0, k1, pad;
+};
+static_assert(offsetof(RunArgs, w) == 96, "kernarg layout: KW at byte 96 (kernarg_consts)");
+typedef const RunArgs* rargs_t;   // generic pointer into the kernarg segment (inferred back to scalar loads)
+__device__ __forceinline__ rargs_t run_args() {
+    const __attribute__((address_space(4))) RunArgs* p =
+        (const __attribute__((address_space(4))) RunArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (rargs_t)p;
+}
+
+__device__ __forceinline__ void lane_fence() {   // this lane's stores visible to its own later loads
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+}
+
+template <bool U0Z>
+__global__ __launch_bounds__(BLK, 4) void k_nt_run(RunArgs args) {
+    constexpr bool BAND = GYM_RUN_BAND == 1;
+    const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
+    if (l >= args.B) return;
+    // Nothing but the lane index, the iteration counter and the lane's status stays live across a pass: J, dJ,
+    // max|sigma| and x_0 are re-read from memory where needed (once per iteration).
+    int st = run_args()->status[l];
+    for (int k = run_args()->k0; st == GYM_ACTIVE && k < run_args()->k1; ++k) {
+        if (GYM_RUN_BAND == 2) {
+            switch ((k >> 1) & 3) {
+                case 0: __builtin_amdgcn_s_setprio(3); break;
+                case 1: __builtin_amdgcn_s_setprio(2); break;
+                case 2: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+        }
+        const int cb = k & 1;
+        {
+            const rargs_t R = run_args();
+            double d, s;
+            backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1, R->cs,
+                                                        R->a.gamma0, l, R->Bp, R->N, d, s);
+            const rargs_t Q = run_args();
+            Q->dJ[l] = d;
+            Q->smax[l] = s;
+            if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = s;
+        }
+        lane_fence();
+        double Jn;
+        {
+            const rargs_t R = run_args();
+            const double2 xa = R->x[cb][wix(0, 0, 2, l, R->Bp)], xb = R->x[cb][wix(0, 1, 2, l, R->Bp)];
+            Jn = rollout_cform<true, U0Z, false, false, kNT, BAND>(R->m, R->w, R->u[cb], R->K1, R->cs, R->xr, R->ur,
+                                                                   R->x[cb ^ 1], R->u[cb ^ 1], R->a.gamma0,
+                                                                   R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y, xb.x, xb.y);
+        }
+        const rargs_t R = run_args();
+        double g = R->a.gamma0;
+        int nr = 1;
+        bool ok = Jn < R->cost[l] + R->a.c * g * R->dJ[l];   // strict Armijo test (:361)
+        if (!ok && R->a.max_ls > 1) {
+            // sigma1 of this sweep (not streamed): the sweep re-run, same code and inputs -> the same bits
+            {
+                const rargs_t P = run_args();
+                double d2, s2;
+                backward_solver_lane<U0Z, OUT_SIGMA, BAND>(P->m, P->w, P->x[cb], P->u[cb], P->xr, P->ur, P->K1,
+                                                           P->cs, 0.0, l, P->Bp, P->N, d2, s2);
+            }
+            lane_fence();
+            for (int j = 1; !ok && j < run_args()->a.max_ls; ++j) {
+                const rargs_t P = run_args();
+                g *= P->a.beta;   // gamma_i *= beta, sequentially (:365)
+                const double2 xa = P->x[cb][wix(0, 0, 2, l, P->Bp)], xb = P->x[cb][wix(0, 1, 2, l, P->Bp)];
+                Jn = rollout_cform<true, U0Z, true, false, kNT, BAND>(P->m, P->w, P->u[cb], P->K1, P->cs, P->xr,
+                                                                      P->ur, P->x[cb ^ 1], P->u[cb ^ 1], g,
+                                                                      P->a.gamma0, l, P->Bp, P->N, xa.x, xa.y, xb.x,
+                                                                      xb.y);
+                ++nr;
+                const rargs_t Q = run_args();
+                ok = Jn < Q->cost[l] + Q->a.c * g * Q->dJ[l];
+            }
+        }
+        const rargs_t F = run_args();
+        F->n_roll[l] += nr;
+        F->n_iter[l] += 1;
+        SolverCtl c = F->a;
+        c.k = k;
+        if (ok) {
+            const double s = F->smax[l];
+            accept_lane(c, l, Jn, g, s, F->cost, F->gamma, F->status, F->res_buf, F->hist_cost, F->Bp);
+            if (s < c.tol) st = GYM_CONVERGED;
+        } else {
+            fail_lane(c, l, F->status, F->res_buf);
+            st = GYM_LS_FAILED;
+        }
+        lane_fence();   // the candidate buffer is the next sweep's input
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Armijo gamma sweeps (plot_armijo_line_search :254-265): J(gamma_g) of the candidate rollout for G step
 // sizes per lane, cost only, one thread per (lane, g).  The G blocks of one lane group re-read the same
 // streams, so a group's blocks are mapped onto one XCD (blocks are dealt round-robin over the 8 XCDs) and
@@ -1687,6 +1837,35 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
     if (p >= 1)  // the trial half's retries and statistics; H1 closes the iteration: total = H0 + H1
         launch_post_trial(m, w, a, b, c, io, rt, b->counters + ht, b->stats + 8 + 8 * ht,
                           ht ? b->stats + 8 : nullptr, ht ? b->stats : nullptr, st);
+    return launch_status();
+}
+
+int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k0,
+                   int32_t k1, void* s) {
+    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT)) return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
+    const bool hist = a->record_history != 0;
+    const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k0, b->hist_len, 0};
+    if (k1 > k0) {
+        TimedLaunch tl(b->timing, 8, st);
+        RunArgs ra;
+        ra.m = Dyn(*m);
+        ra.w = kw(*w);
+        ra.a = c;
+        for (int i = 0; i < 2; ++i) { ra.x[i] = (double2*)b->x[i]; ra.u[i] = b->u[i]; }
+        ra.K1 = (double2*)b->K1; ra.cs = b->cs; ra.xr = b->x_ref; ra.ur = b->u_ref;
+        ra.cost = b->cost; ra.dJ = b->dJ; ra.smax = b->smax; ra.gamma = b->gamma;
+        ra.status = b->status; ra.n_iter = b->n_iter; ra.res_buf = b->res_buf; ra.n_roll = b->n_roll;
+        ra.hist_cost = hist ? b->hist_cost : nullptr; ra.hist_smax = hist ? b->hist_smax : nullptr;
+        ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.pad = 0;
+        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
+    }
+    // the statistics after iteration k1 - 1 ("lanes that ran" = the lanes that executed it; [4] = 0: this
+    // schedule keeps no retry list)
+    hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
+                       b->n_iter, b->n_roll, b->partials, Range{0, b->B}, (int)k1 - 1);
+    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64 * NSTAT), 0, st, b->partials, b->counters, b->stats,
+                       (const double*)nullptr, (double*)nullptr, STAT_BLOCKS);
     return launch_status();
 }
 

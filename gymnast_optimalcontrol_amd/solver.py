@@ -14,7 +14,9 @@ first accepted one -- the same decision the sequential search makes.
 Schedules: ``serial`` launches the backward sweep and the trial of all lanes one after the other
 (gym_newton_iteration); ``pipelined`` splits the lanes into two halves offset by one phase and runs
 one half's (HBM-bound) sweep beside the other half's (fp64-VALU-bound) trial in a single launch
-(gym_newton_phase).  Per lane the arithmetic is identical; only the overlap differs.
+(gym_newton_phase); ``persistent`` runs every lane's iterations back to back inside one launch per
+``chunk`` iterations (gym_newton_run): lanes are independent problems, so no grid-wide step separates
+one iteration from the next.  Per lane the arithmetic is identical; only the overlap differs.
 
 Streams per stage: the sweep reads x (2 pairs) + u (2 planes) and writes K row 1 (2 pairs) +
 (c1, sigma1); the trial reads those + u0 and writes x_new, u_new.  When u_ref[:,0] == 0 (the headline
@@ -66,15 +68,26 @@ class BatchedNewtonSolver:
     # 98,304 on; below that the solve is latency-bound and the two phases per iteration cost more than they
     # overlap).  In units of lanes per compute unit (4 SIMDs x 64 lanes x 1.25).
     PIPELINE_MIN_LANES_PER_CU = 320
+    # The persistent schedule (one launch per solve: no per-iteration launches, statistics or host round trips)
+    # is ahead while the batch is latency-bound well below one wavefront per SIMD (same-box A/B: +16% at 4,096
+    # lanes = BASELINE cfg 2, +10% at 16,384, +4% at 24,576, even at 32,768, 10% behind serial at 65,536;
+    # profiles/r01_ab_persistent.log).
+    PERSISTENT_MAX_LANES_PER_CU = 96
 
     @staticmethod
     def pipeline_min_lanes(device) -> int:
         n_cu = torch.cuda.get_device_properties(device).multi_processor_count
         return BatchedNewtonSolver.PIPELINE_MIN_LANES_PER_CU * n_cu
 
+    @staticmethod
+    def persistent_max_lanes(device) -> int:
+        n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+        return BatchedNewtonSolver.PERSISTENT_MAX_LANES_PER_CU * n_cu
+
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
-                 u0_zero: bool | None = None, checkpoint: bool = False):
+                 u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
+                 chunk: int = 0):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         self.eng = engine
@@ -119,7 +132,14 @@ class BatchedNewtonSolver:
         # and the sweep re-integrates the rest -- bit-identical results, 48 B/stage less traffic, but +0.75 RK4
         # per sweep stage: on MI355X the solver is as VALU- as HBM-limited and this measured 13% slower
         self.checkpoint = bool(checkpoint)
-        b.flags = (_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0)
+        # persistent schedule (gym_newton_run): not combined with checkpointing (its sweep re-integrates blocks)
+        if persistent and self.checkpoint:
+            raise ValueError("the persistent schedule does not support state checkpointing")
+        if persistent is None:   # automatic only when the caller chose no schedule at all
+            persistent = pipeline is None and self.B <= self.persistent_max_lanes(dev)
+        self.persistent = bool(persistent) and not self.checkpoint
+        self.chunk = int(chunk)          # iterations per persistent launch (0: all of max_iters in one)
+        b.flags =(_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0)
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
         for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
@@ -176,8 +196,13 @@ class BatchedNewtonSolver:
         _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
-        if self.pipeline and (self.max_iters is None or self.max_iters > 0):
+        if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
+
+    def _run(self, k0: int, k1: int):
+        _lib.check(self.eng.lib.gym_newton_run(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
+                                               C.byref(self.batch), int(k0), int(k1), self.eng.stream),
+                   "gym_newton_run")
 
     def _phase(self, p: int, do_backward: bool):
         _lib.check(self.eng.lib.gym_newton_phase(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
@@ -187,8 +212,10 @@ class BatchedNewtonSolver:
     def iteration(self) -> torch.Tensor:
         """Enqueue outer iteration k for every active lane; returns the 8 total statistics (device)."""
         k = self.k
-        if self.pipeline:
-            more = self.max_iters is None or k + 1 < self.max_iters
+        if self.persistent:
+            self._run(k, k + 1)
+        elif self.pipeline:
+            more =self.max_iters is None or k + 1 < self.max_iters
             self._phase(2 * k + 1, True)         # sweep H1 (iteration k) beside trial H0 (iteration k)
             self._phase(2 * k + 2, more)         # sweep H0 (iteration k+1) beside trial H1 (iteration k)
         else:
@@ -258,19 +285,49 @@ class BatchedNewtonSolver:
         t0 = time.perf_counter()
         self.max_iters = int(max_iters)
         self.init(x0)
-        log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every, log_every=log_every,
-                          keep_stats=keep_stats)
+        if self.persistent:
+            log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
+        else:
+            log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every,
+                              log_every=log_every, keep_stats=keep_stats)
         x, u, K, s = self.finalize()
         torch.cuda.synchronize(self.eng.device)
         secs = time.perf_counter() - t0
         B = self.B
         n_iter = self.n_iter[:B].clone()
+        # persistent: the lanes' own iteration counts (no lock-step outer loop); otherwise the loop's count
+        iters = int(n_iter.max().item()) if self.persistent else self.k
         return SolveResult(
             x=x, u=u, K=K, sigma=s, cost=self.cost[:B].clone(), n_iter=n_iter, status=self.status[:B].clone(),
-            n_rollouts=self.n_roll[:B].clone(), gamma=self.gamma[:B].clone(), iterations=self.k,
+            n_rollouts=self.n_roll[:B].clone(), gamma=self.gamma[:B].clone(), iterations=iters,
             lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log,
             hist_cost=None if self.hist_cost is None else self.hist_cost[:, :B].clone(),
             hist_smax=None if self.hist_smax is None else self.hist_smax[:, :B].clone())
+
+
+def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_every: int, keep_stats: bool):
+    """Persistent schedule: launches of ``chunk`` iterations (all of max_iters by default); after each one the
+    statistics are all-reduced across ranks (``reduce_stats``) and read, and the loop stops when no lane of any
+    rank is active."""
+    log = []
+    chunk = solver.chunk if solver.chunk > 0 else max(int(max_iters), 1)
+    k = 0
+    while k < max_iters:
+        k1 = min(int(max_iters), k + chunk)
+        solver._run(k, k1)
+        solver.k = k = k1
+        st = solver.stats[:8]
+        if reduce_stats is not None:
+            st = reduce_stats(st)
+        host = st.cpu().numpy()
+        solver.collect_timing()
+        if keep_stats:
+            log.append(host.copy())
+        if log_every:
+            print(f"iter {k}: active={int(host[0])} sumJ={host[1]:.6e} ran={int(host[3])}", flush=True)
+        if host[0] == 0:
+            break
+    return log
 
 
 def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,
@@ -303,10 +360,11 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
 
 def newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                        max_ls=MAX_LINE_SEARCH_ITERS, engine: AcrobotEngine | None = None, hist_len=0,
-                       reduce_stats=None, pipeline: bool | None = None) -> SolveResult:
+                       reduce_stats=None, pipeline: bool | None = None,
+                       persistent: bool | None = None) -> SolveResult:
     """Batched newton_Algorithm: x0 (B,4) -> SolveResult (device tensors)."""
     eng = engine or AcrobotEngine()
     x0 = eng.t(x0).reshape(-1, 4)
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, x0.shape[0], tol=tol, beta=beta, c=c, gamma_0=gamma_0,
-                                 max_ls=max_ls, hist_len=hist_len, pipeline=pipeline)
+                                 max_ls=max_ls, hist_len=hist_len, pipeline=pipeline, persistent=persistent)
     return solver.solve(x0, max_iters, reduce_stats=reduce_stats)

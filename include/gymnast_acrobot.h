@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 4
+#define GYM_ABI_VERSION 5
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -92,8 +92,9 @@ typedef struct gym_armijo {
 /* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
  * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
  * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p), 7 sigma1 re-run of the lanes that
- * backtrack.  A pair is recorded only if the previous one of its kind was collected. */
-#define GYM_NK 8
+ * backtrack, 8 persistent run (gym_newton_run).  A pair is recorded only if the previous one of its kind was
+ * collected. */
+#define GYM_NK 9
 typedef struct gym_timing {
     void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
     double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
@@ -212,6 +213,14 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
 int gym_newton_pipeline_split(const gym_batch* bt, int64_t* Bh);
 int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t p,
                      int32_t do_backward, void* stream);
+/* Persistent schedule: ONE launch in which every lane still ACTIVE runs its own outer iterations k0 .. k1-1 back to
+ * back (newton_Algorithm :329-396 per lane: sweep, Armijo trial 1, and for a lane that rejects it the sigma1 re-run
+ * and trials 2..max_ls in sequence), stopping at convergence or LS failure; then the statistics of iteration k1-1
+ * into stats[0,8) ([4] = 0: no retry list is kept).  Lanes need no grid-wide step between iterations, so there is
+ * none.  Same per-lane arithmetic as gym_newton_iteration / gym_newton_phase (bit-identical results).  k0 = the
+ * iterations every active lane has done (0 after gym_newton_init).  Not with GYM_FLAG_X_CKPT (GYM_EINVAL). */
+int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t k0,
+                   int32_t k1, void* stream);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
  * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
  * (sigma0 recomputed from that iteration's u0).  Any output may be NULL.  With GYM_FLAG_X_CKPT the result

@@ -247,9 +247,9 @@ def test_ragged_batches_and_padding(B, task2_refs):
     assert last[1] == pytest.approx(o["cost"].sum(), rel=1e-10)
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("schedule", ["serial", "pipelined", "persistent"])
 @pytest.mark.parametrize("max_iters", [12, 120])
-def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, pipeline, max_iters):
+def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, schedule, max_iters):
     """K and sigma of each lane's last iteration (newton_Algorithm's return values) after backtracking, LS
     failures, a NaN lane and the max_iters cut-off.  sigma1 is not streamed by the solver: gym_newton_sigma
     re-runs each lane's last sweep from the state buffer that iteration started from, and the lanes that
@@ -263,7 +263,8 @@ def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, pipeline, max_iter
     x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
     x0[:20, 2:] = np.random.default_rng(6).uniform(-2.0, 2.0, (20, 2))      # seed-14-like lanes: early LS failures
     x0[9] = np.nan
-    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=1.0, pipeline=pipeline).solve(x0, max_iters)
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=1.0, pipeline=schedule == "pipelined",
+                            persistent=schedule == "persistent").solve(x0, max_iters)
     o = c_oracle.newton_solve(x0, xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=1.0)
     ni, st = r.n_iter.cpu().numpy(), r.status.cpu().numpy()
     same = (ni == o["n_iter"]) & (st == o["status"]) & (r.n_rollouts.cpu().numpy() == o["n_rollouts"])
@@ -312,7 +313,8 @@ def test_u_ref_trim_and_errors(tg, task2_refs):
         tg.newton_Algorithm(np.zeros(4), xr, ur[:-3], max_iters=3)
 
 
-def test_full_size_properties(task2_refs):
+@pytest.mark.parametrize("persistent", [False, True])
+def test_full_size_properties(task2_refs, persistent):
     """BASELINE cfg 3 size (262,144 lanes): the golden lane 0 within 1e-8, every headline lane converges
     in the reference's iteration band, stats are consistent."""
     from gymnast_optimalcontrol_amd import _lib
@@ -321,14 +323,19 @@ def test_full_size_properties(task2_refs):
     xr, ur, _ = task2_refs
     B = 262144
     x0 = np.zeros((B, 4)); x0[1:, :2] = np.random.default_rng(0).uniform(-0.5, 0.5, (B - 1, 2))
-    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1).solve(x0, 5000, keep_stats=True)
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=0.1,
+                            persistent=persistent).solve(x0, 5000, keep_stats=True)
     from conftest import load_golden
     ref = load_golden("task2_reference_output")
     assert rel_l2(r.x[0].cpu().numpy(), ref["x"]) < TOL_TRAJ
     st = r.status.cpu().numpy(); n = r.n_iter.cpu().numpy()
     assert (st == _lib.CONVERGED).all()
     assert 370 <= n.min() and n.max() <= 420
-    assert r.lane_iterations == int(n.sum()) == int(sum(s[3] for s in r.stats_log))
+    assert r.lane_iterations == int(n.sum())
+    if not persistent:   # one statistics row per iteration: "lanes that ran" sums to the lane-iterations
+        assert r.lane_iterations == int(sum(s[3] for s in r.stats_log))
+    else:
+        assert r.stats_log[-1][0] == 0 and r.stats_log[-1][5] == B
 
 
 @pytest.mark.parametrize("max_iters", [25, 5000])
@@ -354,6 +361,46 @@ def test_pipelined_schedule_matches_serial(task2_refs, max_iters):
     if max_iters == 5000:
         assert (rs.status.cpu().numpy() == 2).sum() >= 2        # the batch exercises LS failures
         assert ls[:, 4].sum() > 0                               # ... and Armijo retries
+
+
+@pytest.mark.parametrize("max_iters,chunk,u0z", [(25, 0, True), (5000, 0, True), (5000, 7, False), (5000, 0, False)])
+def test_persistent_schedule_matches_serial(task2_refs, max_iters, chunk, u0z):
+    """The persistent schedule (gym_newton_run: each lane's iterations back to back in one launch per chunk, its
+    Armijo trials 2..max_ls sequential) gives bitwise the serial schedule's lanes -- trajectories, last-iteration
+    K and sigma, costs, decisions, rollout counts, per-lane histories -- incl. backtracking / LS-failure / NaN
+    lanes, the max_iters cut-off and chunked launches."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    B = 1000
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(21).uniform(-1.5, 1.5, (B, 2))
+    x0[7] = np.nan
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, u0_zero=None if u0z else False, hist_len=64)
+    rs = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, **kw).solve(x0, max_iters, keep_stats=True)
+    rr = BatchedNewtonSolver(eng, xr, ur, B, persistent=True, chunk=chunk, **kw).solve(x0, max_iters, keep_stats=True)
+    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax"):
+        a, b = getattr(rs, name).cpu().numpy(), getattr(rr, name).cpu().numpy()
+        assert np.array_equal(a, b, equal_nan=True), name
+    assert rs.iterations == rr.iterations
+    last_s, last_r = rs.stats_log[-1], rr.stats_log[-1]
+    np.testing.assert_array_equal(last_s[[0, 5, 6, 7]], last_r[[0, 5, 6, 7]])   # active, converged, failed, rollouts
+    np.testing.assert_allclose(last_s[1], last_r[1], rtol=1e-12)                 # sum J (summation order differs)
+    st = rr.status.cpu().numpy()
+    if max_iters == 5000:
+        assert (st == _lib.LS_FAILED).sum() >= 2 and st[7] == _lib.LS_FAILED
+        assert (rr.n_rollouts.cpu().numpy() > rr.n_iter.cpu().numpy()).sum() > 0   # Armijo retries happened
+    else:
+        assert (st == _lib.MAX_ITERS).any()
+
+
+def test_persistent_schedule_refuses_checkpointing(task2_refs):
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    with pytest.raises(ValueError):
+        BatchedNewtonSolver(AcrobotEngine(), xr, ur, 8, persistent=True, checkpoint=True)
 
 
 @pytest.mark.parametrize("pipeline", [False, True])

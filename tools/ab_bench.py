@@ -2,7 +2,7 @@
 """Interleaved A/B timing of library variants in ONE process on one device (measurement tool).
 
     python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so:serial lib_b.so:pipe:nou0z ...
-(":serial" / ":pipe" select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":nock" the state
+(":serial" / ":pipe" / ":run" (persistent) select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":nock" the state
 checkpointing; default:
 the solver's choice)
 Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
@@ -36,7 +36,7 @@ def main():
     from gymnast_optimalcontrol_amd import _lib
     def split(spec):
         path, *opts = spec.split(":")
-        sched = {"serial": False, "pipe": True}
+        sched = {"serial": False, "pipe": True, "run": "run"}
         return (os.path.abspath(path), next((sched[o] for o in opts if o in sched), None), "nou0z" not in opts,
                 "nock" not in opts)
     eng = AcrobotEngine(lib_path=split(a.libs[0])[0])
@@ -50,16 +50,20 @@ def main():
         for p in a.libs:
             eng.lib = libs[p]
             _, sched, u0z, ck = split(p)
-            s.pipeline = default_pipe if sched is None else sched
+            s.persistent = sched == "run"
+            s.pipeline = default_pipe if sched in (None, "run") else sched
             s.u0_zero = default_u0z and u0z
-            s.checkpoint = ck
-            s.batch.flags = (_lib.FLAG_U0_ZERO if s.u0_zero else 0) | (_lib.FLAG_X_CKPT if ck else 0)
+            s.checkpoint = ck and not s.persistent
+            s.batch.flags = (_lib.FLAG_U0_ZERO if s.u0_zero else 0) | (_lib.FLAG_X_CKPT if s.checkpoint else 0)
             s.reset_timing()
             out = s.solve(xd, a.max_iters)
             kt = s.kernel_times()
             if r == 0:
                 continue   # warm-up round
-            if kt["backward"][1]:
+            if kt["run"][1]:     # persistent: the run launch(es) as "bwd", nothing as "trial"
+                res[p]["bwd"].append(kt["run"][0] / kt["run"][1])
+                res[p]["trial"].append(0.0)
+            elif kt["backward"][1]:
                 res[p]["bwd"].append(kt["backward"][0] / kt["backward"][1])
                 res[p]["trial"].append(kt["trial"][0] / kt["trial"][1])
             else:   # pipelined: report the phase pair as "bwd" (odd) / "trial" (even)
