@@ -287,20 +287,14 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         q.u0 = U0Z ? 0.0 : bld1<CP>(rsrc(Ub + (int64_t)t * row), o1, 0);
     };
     const gym::PolyRegs pk = gym::poly_vgprs();   // loop-invariant coefficients held in VGPRs
-    TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
-    fetch(pre, 0);
-    pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
-    prio_start<BAND ? 1 : PRIO_NONE>();
-    for (int t = 0; t < T; ++t) {
+    // stage t with its streams in q (prefetched earlier)
+    auto body = [&](const TrialStage& q, int t) {
         prio_band<BAND ? 1 : PRIO_NONE>(t, T);
-        const double2 k0 = pre.k0, k1 = pre.k1;
-        const double cg = pre.cg, s1 = pre.s1, u0 = pre.u0;
-        if (t + 1 < T) fetch(pre, t + 1);
         const double* urt = ur + 2 * t;
-        const double s0 = -(G00 * (u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
-        const double v0 = u0 + gamma * s0;                 // U0Z: u0 = ur0 = 0  =>  v0 = +0 exactly
-        const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
-        const double v1 = SIG ? __builtin_fma(dg, s1, cg + kx) : cg + kx;
+        const double s0 = -(G00 * (q.u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
+        const double v0 = q.u0 + gamma * s0;                 // U0Z: u0 = ur0 = 0  =>  v0 = +0 exactly
+        const double kx = ((q.k0.x * n0 + q.k0.y * n1) + q.k1.x * n2) + q.k1.y * n3;
+        const double v1 = SIG ? __builtin_fma(dg, q.s1, q.cg + kx) : q.cg + kx;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
         J += xcost(ka.w.Q, n0, n1, n2, n3, xr + 4 * t);
@@ -316,6 +310,15 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
             bst2(rX, o2, 0, n0, n1);
             bst2(rX, o2, WROW, n2, n3);
         }
+    };
+    TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
+    fetch(pre, 0);
+    pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
+    prio_start<BAND ? 1 : PRIO_NONE>();
+    for (int t = 0; t < T; ++t) {
+        const TrialStage q = pre;
+        if (t + 1 < T) fetch(pre, t + 1);
+        body(q, t);
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
 }
@@ -1129,30 +1132,81 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_trial(Dyn m, KW w, SolverCtl a, T
 // One pipeline phase: the first nb_b workgroups run the backward sweep of one half, the rest run the
 // Armijo trial of the other half.  The sweep is HBM-bound and the trial fp64-VALU-bound, so co-resident
 // waves of the two kinds overlap memory and arithmetic on every CU.  The two halves' lanes are disjoint.
+// Every operand is in one by-value argument struct, re-read from the kernel-argument segment at each use
+// (phase_args(), as the persistent kernel's run_args()): no pointer or control value is held in SGPRs across
+// the stage loops, where their spills cost v_readlane VALU slots (13 per trial stage before; 1 now;
+// same-box A/B +0.3%).
+struct PhaseArgs {
+    Dyn m;
+    KW w;
+    SolverCtl a;
+    TrialIO io;
+    const double2* xb_in;
+    const double* ub_in;
+    double2* K1;
+    double* cs;
+    const double* xr;
+    const double* ur;
+    double *cost, *dJ, *smax, *gamma;
+    int32_t *status, *n_iter, *res_buf, *n_roll, *retry_list, *counter;
+    double *hist_cost, *hist_smax;
+    Range rb, rt;
+    int64_t Bp;
+    int32_t N, kb, nb_b, pad;
+};
+static_assert(offsetof(PhaseArgs, w) == 96, "kernarg layout: KW at byte 96 (kernarg_consts)");
+typedef const PhaseArgs* pargs_t;
+__device__ __forceinline__ pargs_t phase_args() {
+    const __attribute__((address_space(4))) PhaseArgs* p =
+        (const __attribute__((address_space(4))) PhaseArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (pargs_t)p;
+}
+
 template <bool U0Z, bool CK>
-__global__ __launch_bounds__(BLK, 4) void k_nt_phase(Dyn m, KW w, SolverCtl a, TrialIO io,
-                                                     const double2* __restrict__ xb_in,
-                                                     const double* __restrict__ ub_in, int kb, int nb_b,
-                                                     Range rb, Range rt, double2* __restrict__ K1,
-                                                     double* __restrict__ cs, const double* __restrict__ xr,
-                                                     const double* __restrict__ ur, double* __restrict__ cost,
-                                                     double* __restrict__ dJ, double* __restrict__ smax,
-                                                     double* __restrict__ gamma, int32_t* __restrict__ status,
-                                                     int32_t* __restrict__ n_iter, int32_t* __restrict__ res_buf,
-                                                     int32_t* __restrict__ n_roll, int32_t* __restrict__ retry_list,
-                                                     int32_t* __restrict__ counter, double* __restrict__ hist_cost,
-                                                     double* __restrict__ hist_smax, int64_t Bp, int N) {
+__global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
     GYM_CK_LDS(CK, U0Z);
-    if ((int)blockIdx.x < nb_b) {
-        const int64_t l = rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
-        if (l >= rb.hi || status[l] != GYM_ACTIVE) return;
-        backward_solver<U0Z, CK>(m, w, xb_in, ub_in, xr, ur, K1, cs, a.gamma0, dJ, smax, hist_smax, l, Bp, N, kb,
-                                 a.hist_len, ck_lds);
+    if ((int)blockIdx.x < args.nb_b) {
+        const int64_t l = args.rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
+        if (l >= args.rb.hi || args.status[l] != GYM_ACTIVE) return;
+        double d, s;
+        {
+            const pargs_t R = phase_args();
+            if (CK)
+                backward_solver_lane_ck<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, R->xr, R->ur, R->K1, R->cs,
+                                                         R->a.gamma0, ck_lds, l, R->Bp, R->N, d, s);
+            else
+                backward_solver_lane<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, R->xr, R->ur, R->K1, R->cs,
+                                                      R->a.gamma0, l, R->Bp, R->N, d, s);
+        }
+        const pargs_t Q = phase_args();
+        Q->dJ[l] = d;
+        Q->smax[l] = s;
+        if (Q->hist_smax && Q->kb < Q->a.hist_len) Q->hist_smax[(int64_t)Q->kb * Q->Bp + l] = s;
     } else {
-        const int64_t l = rt.lo + (int64_t)(blockIdx.x - nb_b) * BLK + threadIdx.x;
-        if (l >= rt.hi || status[l] != GYM_ACTIVE) return;
-        trial_solver<U0Z, CK>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
-                              retry_list + rt.lo, counter, hist_cost, l, Bp, N);
+        const int64_t l = args.rt.lo + (int64_t)(blockIdx.x - args.nb_b) * BLK + threadIdx.x;
+        if (l >= args.rt.hi || args.status[l] != GYM_ACTIVE) return;
+        double Jn;
+        {   // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass)
+            const pargs_t R = phase_args();
+            const double2 xa = R->io.x[wix(0, 0, 2, l, R->Bp)], xb = R->io.x[wix(0, 1, 2, l, R->Bp)];
+            Jn = rollout_cform<true, U0Z, false, CK>(R->m, R->w, R->io.u, R->K1, R->cs, R->xr, R->ur, R->io.xn,
+                                                     R->io.un, R->a.gamma0, R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y,
+                                                     xb.x, xb.y);
+        }
+        const pargs_t R = phase_args();
+        const SolverCtl a = R->a;
+        const double g = a.gamma0;
+        R->n_roll[l] += 1;
+        if (Jn < R->cost[l] + a.c * g * R->dJ[l]) {  // strict Armijo test (:361)
+            R->n_iter[l] += 1;
+            accept_lane(a, l, Jn, g, R->smax[l], R->cost, R->gamma, R->status, R->res_buf, R->hist_cost, R->Bp);
+        } else if (a.max_ls > 1) {
+            R->retry_list[R->rt.lo + atomicAdd(R->counter, 1)] = (int32_t)l;
+        } else {
+            R->n_iter[l] += 1;
+            fail_lane(a, l, R->status, R->res_buf);
+        }
     }
 }
 
@@ -1828,11 +1882,19 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
     const TrialIO io = trial_io(b, kt < 0 ? 0 : kt);
     if (nb_b + nb_t > 0) {
         TimedLaunch tl(b->timing, (p & 1) ? 5 : 6, st);
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io,
-                           (const double2*)b->x[kb & 1], b->u[kb & 1], kb, nb_b, rb, rt, (double2*)b->K1,
-                           b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
-                           b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters + ht,
-                           hist ? b->hist_cost : nullptr, hist ? b->hist_smax : nullptr, b->Bp, b->N);
+        PhaseArgs pa;
+        pa.m = Dyn(*m);
+        pa.w = kw(*w);
+        pa.a = c;
+        pa.io = io;
+        pa.xb_in = (const double2*)b->x[kb & 1]; pa.ub_in = b->u[kb & 1];
+        pa.K1 = (double2*)b->K1; pa.cs = b->cs; pa.xr = b->x_ref; pa.ur = b->u_ref;
+        pa.cost = b->cost; pa.dJ = b->dJ; pa.smax = b->smax; pa.gamma = b->gamma;
+        pa.status = b->status; pa.n_iter = b->n_iter; pa.res_buf = b->res_buf; pa.n_roll = b->n_roll;
+        pa.retry_list = b->retry_list; pa.counter = b->counters + ht;
+        pa.hist_cost = hist ? b->hist_cost : nullptr; pa.hist_smax = hist ? b->hist_smax : nullptr;
+        pa.rb = rb; pa.rt = rt; pa.Bp = b->Bp; pa.N = b->N; pa.kb = kb; pa.nb_b = nb_b; pa.pad = 0;
+        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, pa);
     }
     if (p >= 1)  // the trial half's retries and statistics; H1 closes the iteration: total = H0 + H1
         launch_post_trial(m, w, a, b, c, io, rt, b->counters + ht, b->stats + 8 + 8 * ht,
