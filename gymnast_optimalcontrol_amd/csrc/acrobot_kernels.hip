@@ -934,31 +934,80 @@ __global__ void k_pack(const double* __restrict__ src, double* __restrict__ dst,
     for (int k = 0; k < W; ++k) dst[W * d + k] = (lane < B) ? s[k] : 0.0;
 }
 
-__global__ void k_unpack(const double* __restrict__ s0, const double* __restrict__ s1,
-                         const int32_t* __restrict__ sel, double* __restrict__ dst, int64_t B, int64_t Bp, int L,
-                         int C, int W) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // output element index, lane-major
-    const int P = C / W;
-    if (o >= B * L * P) return;
-    const int p = (int)(o % P);
-    const int64_t rest = o / P;
-    const int64_t t = rest % L;
-    const int64_t lane = rest / L;
-    const double* s = (sel && sel[lane]) ? s1 : s0;
-    const double* e = s + W * (W == 2 ? wix(t, p, P, lane, Bp) : (t * P + p) * Bp + lane);
-    for (int k = 0; k < W; ++k) dst[W * o + k] = e[k];
+// SoA -> lane-major transposes through LDS.  One workgroup (256 threads) moves the tile of one 64-lane group x
+// TS knots: the SoA rows are read coalesced (a 64-lane row is 512 B or 1 KiB contiguous), the tile is staged in
+// LDS as [knot][component][lane] with a 65-double row pitch (a lane's column is read conflict-free), and each
+// lane's TS x C output doubles -- contiguous in the lane-major array -- are written by consecutive threads.
+// Src supplies component c of knot t of a lane (which may be derived, e.g. sigma0, or a constant 0).
+constexpr int TILE_PITCH = BLK + 1;
+constexpr int TILE_THREADS = 256;
+constexpr int TILE_DOUBLES = 4096;   // 32 KiB of LDS per workgroup (5 per CU): TS * C * TILE_PITCH <= TILE_DOUBLES
+inline int tile_knots(int C) {
+    int ts = TILE_DOUBLES / (C * TILE_PITCH);
+    return ts < 1 ? 1 : (ts > 32 ? 32 : ts);
 }
 
-__global__ void k_unpack_gains(const double2* __restrict__ K1, double* __restrict__ K, int64_t B, int64_t Bp,
-                               int T) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (lane, t)
-    if (o >= B * T) return;
-    const int64_t t = o % T, lane = o / T;
-    const double2 a = K1[wix(t, 0, 2, lane, Bp)], b = K1[wix(t, 1, 2, lane, Bp)];
-    double* d = K + 8 * o;
-    d[0] = 0.0; d[1] = 0.0; d[2] = 0.0; d[3] = 0.0;
-    d[4] = a.x; d[5] = a.y; d[6] = b.x; d[7] = b.y;
+struct SrcPairs {   // wave-blocked pairs (L, P, Bp) double2, per-lane buffer select
+    const double2 *s0, *s1;
+    const int32_t* sel;
+    int P;
+    __device__ __forceinline__ double operator()(int64_t t, int c, int64_t lane, int64_t Bp) const {
+        const double2* b = (sel && sel[lane]) ? s1 : s0;
+        const double2 v = b[wix(t, c >> 1, P, lane, Bp)];
+        return (c & 1) ? v.y : v.x;
+    }
+};
+struct SrcPlanes {  // planes (L, C, Bp) double, per-lane buffer select
+    const double *s0, *s1;
+    const int32_t* sel;
+    int C;
+    __device__ __forceinline__ double operator()(int64_t t, int c, int64_t lane, int64_t Bp) const {
+        const double* b = (sel && sel[lane]) ? s1 : s0;
+        return b[(t * C + c) * Bp + lane];
+    }
+};
+struct SrcGains {   // full K_t (2,4) from its row 1 (K1 pairs); row 0 is identically 0
+    const double2* K1;
+    __device__ __forceinline__ double operator()(int64_t t, int c, int64_t lane, int64_t Bp) const {
+        if (c < 4) return 0.0;
+        const double2 v = K1[wix(t, (c - 4) >> 1, 2, lane, Bp)];
+        return (c & 1) ? v.y : v.x;
+    }
+};
+struct SrcSigma {   // sigma of each lane's last iteration: sigma0 recomputed from that iteration's u0, sigma1 plane
+    KW w;
+    const double *cs, *u0b, *u1b, *ur;
+    const int32_t* n_iter;
+    __device__ __forceinline__ double operator()(int64_t t, int c, int64_t lane, int64_t Bp) const {
+        const int it = n_iter[lane];
+        if (it <= 0) return 0.0;
+        if (c == 1) return cs[pix((int)t, 1, 2, lane, Bp)];
+        const double* u = ((it - 1) & 1) ? u1b : u0b;
+        return -(w.G00 * (u[pix((int)t, 0, 2, lane, Bp)] - ur[2 * t])) * w.iG00;
+    }
+};
+
+// dst (B, L, C) lane-major; grid (Bp / 64) x ceil(L / TS); dynamic LDS TS * C * TILE_PITCH doubles
+template <class Src>
+__global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* __restrict__ dst, int64_t B,
+                                                               int64_t Bp, int L, int C, int TS) {
+    extern __shared__ double tile[];
+    const int64_t g0 = (int64_t)blockIdx.x * BLK;          // first lane of the group
+    const int t0 = (int)blockIdx.y * TS;
+    const int ts = (L - t0 < TS) ? L - t0 : TS;
+    const int rows = ts * C;
+    for (int i = threadIdx.x; i < rows * BLK; i += TILE_THREADS) {
+        const int ln = i & (BLK - 1), r = i >> 6;          // r = knot * C + component
+        tile[r * TILE_PITCH + ln] = src(t0 + r / C, r % C, g0 + ln, Bp);
+    }
+    __syncthreads();
+    const int64_t nl = (B - g0 < BLK) ? B - g0 : BLK;      // real lanes of the group
+    for (int i = threadIdx.x; i < nl * rows; i += TILE_THREADS) {
+        const int ln = i / rows, r = i - ln * rows;
+        dst[((g0 + ln) * L + t0) * C + r] = tile[r * TILE_PITCH + ln];
+    }
 }
+
 
 // ------------------------------------------------------------------------------------------
 // kernels: batched Newton / Armijo solver (newton_Algorithm :298-398)
@@ -1554,27 +1603,6 @@ __global__ void k_finalize_status(int32_t* __restrict__ status, int32_t* __restr
     }
 }
 
-// sigma of each lane's last iteration, lane-major (B,T,2): sigma1 from the sigma1 plane (k_nt_sigma re-ran the
-// lane's last sweep into it), sigma0 = -(2R0 (u0 - ur0)) / (2R0) recomputed from that iteration's controls,
-// buffer (n_iter-1) & 1.
-__global__ void k_finalize_sigma(KW w, const double* __restrict__ cs, const double* __restrict__ u0b,
-                                 const double* __restrict__ u1b, const double* __restrict__ ur,
-                                 const int32_t* __restrict__ n_iter, double* __restrict__ sig, int64_t B, int64_t Bp,
-                                 int T) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (lane, t)
-    if (o >= B * T) return;
-    const int t = (int)(o % T);
-    const int64_t lane = o / T;
-    const int it = n_iter[lane];
-    double s0 = 0.0, s1 = 0.0;
-    if (it > 0) {
-        const double* u = ((it - 1) & 1) ? u1b : u0b;
-        s0 = -(w.G00 * (u[pix(t, 0, 2, lane, Bp)] - ur[2 * t])) * w.iG00;
-        s1 = cs[pix(t, 1, 2, lane, Bp)];
-    }
-    sig[2 * o] = s0;
-    sig[2 * o + 1] = s1;
-}
 
 // GYM_FLAG_X_CKPT: rebuild every knot of a state buffer from x_0 and the tau2 controls, x_{t+1} =
 // RK4(x_t, u1_t) -- the same recursion (and code) the trial ran, so the rebuilt knots equal the bits it
@@ -1626,6 +1654,16 @@ inline bool bad_dims(int64_t B, int64_t Bp, int N) {
 }
 
 inline int launch_status() { return (int)hipGetLastError(); }
+
+template <class Src>
+int launch_unpack_tiled(const Src& src, double* dst, int64_t B, int64_t Bp, int L, int C, hipStream_t st) {
+    const int ts = tile_knots(C);
+    if (C * TILE_PITCH > TILE_DOUBLES) return GYM_EINVAL;
+    const dim3 grid((unsigned)(Bp / BLK), (unsigned)((L + ts - 1) / ts));
+    hipLaunchKernelGGL(k_unpack_tiled<Src>, grid, dim3(TILE_THREADS), sizeof(double) * ts * C * TILE_PITCH, st, src,
+                       dst, B, Bp, L, C, ts);
+    return launch_status();
+}
 
 inline Mat4 mat4(const double* p) { Mat4 m; for (int i = 0; i < 16; ++i) m.v[i] = p[i]; return m; }
 inline Mat2 mat2(const double* p) { Mat2 m; for (int i = 0; i < 4; ++i) m.v[i] = p[i]; return m; }
@@ -1694,17 +1732,15 @@ int gym_unpack_lanes(const double* s0, const double* s1, const int32_t* sel, dou
                      int32_t L, int32_t C, int32_t W, void* s) {
     if (!s0 || !dst || bad_dims(B, Bp, 2) || L <= 0 || C <= 0 || (W != 1 && W != 2) || (C % W) || (sel && !s1))
         return GYM_EINVAL;
-    const int64_t n = B * L * (C / W);
-    hipLaunchKernelGGL(k_unpack, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)s, s0, s1 ? s1 : s0, sel, dst, B,
-                       Bp, L, C, W);
-    return launch_status();
+    if (W == 2)
+        return launch_unpack_tiled(SrcPairs{(const double2*)s0, (const double2*)(s1 ? s1 : s0), sel, C / 2}, dst, B,
+                                   Bp, L, C, (hipStream_t)s);
+    return launch_unpack_tiled(SrcPlanes{s0, s1 ? s1 : s0, sel, C}, dst, B, Bp, L, C, (hipStream_t)s);
 }
 
 int gym_unpack_gains(const double* K1, double* K, int64_t B, int64_t Bp, int32_t T, void* s) {
     if (!K1 || !K || bad_dims(B, Bp, 2) || T <= 0) return GYM_EINVAL;
-    hipLaunchKernelGGL(k_unpack_gains, dim3(grid_for(B * T, 256)), dim3(256), 0, (hipStream_t)s, (const double2*)K1, K,
-                       B, Bp, T);
-    return launch_status();
+    return launch_unpack_tiled(SrcGains{(const double2*)K1}, K, B, Bp, T, 8, (hipStream_t)s);
 }
 
 int gym_rollout_open_loop(const gym_model* m, const gym_weights* w, const double* x0, const double* u,
@@ -1967,9 +2003,8 @@ int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* 
         const int e = launch_status();
         if (e) return e;
     }
-    hipLaunchKernelGGL(k_finalize_sigma, dim3(grid_for(b->B * T, 256)), dim3(256), 0, st, kw(*w),
-                       (const double*)b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter, sig_out, b->B, b->Bp, T);
-    return launch_status();
+    return launch_unpack_tiled(SrcSigma{kw(*w), b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter}, sig_out, b->B, b->Bp,
+                               T, 2, st);
 }
 
 static int sweep_grid(int64_t Bp, int G) {

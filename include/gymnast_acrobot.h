@@ -154,7 +154,8 @@ int gym_stage_cost_derivs(const double* x, const double* xr, const double* u, co
  * zero-filled.  Here and below "(L,P,Bp) pairs" names the wave-blocked pair layout of the Layouts note. */
 int gym_pack_lanes(const double* src, double* dst, int64_t B, int64_t Bp, int32_t L, int32_t C, int32_t W,
                    void* stream);
-/* SoA -> lane-major; if sel != NULL lane b reads from (sel[b] ? src1 : src0). */
+/* SoA -> lane-major; if sel != NULL lane b reads from (sel[b] ? src1 : src0).  Tiled through LDS (64 lanes x a few
+ * knots per workgroup: coalesced reads and writes); C <= 63 components per knot (GYM_EINVAL otherwise). */
 int gym_unpack_lanes(const double* src0, const double* src1, const int32_t* sel, double* dst, int64_t B, int64_t Bp,
                      int32_t L, int32_t C, int32_t W, void* stream);
 /* compact gains K1 (T,2,Bp) -> full lane-major K (B,T,2,4) with row 0 = 0 */
