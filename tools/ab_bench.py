@@ -3,7 +3,7 @@
 
     python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so:serial lib_b.so:pipe:nou0z ...
 (":serial" / ":pipe" / ":run" (persistent) select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":nock" the state
-checkpointing; default:
+checkpointing, ":noreorder" the Morton-order lane grouping of solve(); default:
 the solver's choice)
 Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
 kernel library is swapped), so buffer placement -- worth +-4% on its own -- is held fixed; prints
@@ -38,7 +38,7 @@ def main():
         path, *opts = spec.split(":")
         sched = {"serial": False, "pipe": True, "run": "run"}
         return (os.path.abspath(path), next((sched[o] for o in opts if o in sched), None), "nou0z" not in opts,
-                "nock" not in opts)
+                "nock" not in opts, "noreorder" not in opts)
     eng = AcrobotEngine(lib_path=split(a.libs[0])[0])
     s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1).enable_timing()
     default_pipe = s.pipeline
@@ -49,7 +49,8 @@ def main():
     for r in range(a.rounds + 1):
         for p in a.libs:
             eng.lib = libs[p]
-            _, sched, u0z, ck = split(p)
+            _, sched, u0z, ck, reorder = split(p)
+            s.reorder = reorder
             s.persistent = sched == "run"
             s.pipeline = default_pipe if sched in (None, "run") else sched
             s.u0_zero = default_u0z and u0z
