@@ -30,7 +30,7 @@ EXPORTS = (
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run")
 
-ABI_VERSION = 5         # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 6         # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
@@ -66,7 +66,7 @@ class GymBatch(C.Structure):
                 ("flags", C.c_int32), ("pad", C.c_int32), ("x", _P * 2), ("u", _P * 2), ("K1", _P), ("cs", _P), ("x_ref", _P), ("u_ref", _P),
                 ("cost", _P), ("dJ", _P), ("smax", _P), ("gamma", _P), ("status", _P), ("n_iter", _P),
                 ("res_buf", _P), ("n_roll", _P), ("retry_list", _P), ("counters", _P), ("cand_ok", _P),
-                ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P),
+                ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P), ("lane_map", _P),
                 ("timing", C.POINTER(GymTiming))]
 
 

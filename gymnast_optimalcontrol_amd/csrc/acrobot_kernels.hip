@@ -989,7 +989,8 @@ struct SrcSigma {   // sigma of each lane's last iteration: sigma0 recomputed fr
 
 // dst (B, L, C) lane-major; grid (Bp / 64) x ceil(L / TS); dynamic LDS TS * C * TILE_PITCH doubles
 template <class Src>
-__global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* __restrict__ dst, int64_t B,
+__global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* __restrict__ dst,
+                                                               const int64_t* __restrict__ map, int64_t B,
                                                                int64_t Bp, int L, int C, int TS) {
     extern __shared__ double tile[];
     const int64_t g0 = (int64_t)blockIdx.x * BLK;          // first lane of the group
@@ -1004,7 +1005,8 @@ __global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* 
     const int64_t nl = (B - g0 < BLK) ? B - g0 : BLK;      // real lanes of the group
     for (int i = threadIdx.x; i < nl * rows; i += TILE_THREADS) {
         const int ln = i / rows, r = i - ln * rows;
-        dst[((g0 + ln) * L + t0) * C + r] = tile[r * TILE_PITCH + ln];
+        const int64_t row = map ? map[g0 + ln] : g0 + ln;   // output lane (the caller's order)
+        dst[(row * L + t0) * C + r] = tile[r * TILE_PITCH + ln];
     }
 }
 
@@ -1656,12 +1658,13 @@ inline bool bad_dims(int64_t B, int64_t Bp, int N) {
 inline int launch_status() { return (int)hipGetLastError(); }
 
 template <class Src>
-int launch_unpack_tiled(const Src& src, double* dst, int64_t B, int64_t Bp, int L, int C, hipStream_t st) {
+int launch_unpack_tiled(const Src& src, double* dst, int64_t B, int64_t Bp, int L, int C, hipStream_t st,
+                        const int64_t* map = nullptr) {
     const int ts = tile_knots(C);
     if (C * TILE_PITCH > TILE_DOUBLES) return GYM_EINVAL;
     const dim3 grid((unsigned)(Bp / BLK), (unsigned)((L + ts - 1) / ts));
     hipLaunchKernelGGL(k_unpack_tiled<Src>, grid, dim3(TILE_THREADS), sizeof(double) * ts * C * TILE_PITCH, st, src,
-                       dst, B, Bp, L, C, ts);
+                       dst, map, B, Bp, L, C, ts);
     return launch_status();
 }
 
@@ -1985,9 +1988,15 @@ int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batc
     if (e) return e;
     const int T = b->N - 1;
     if (x_out && (e = gym_newton_fill_states(m, b, -1, s))) return e;
-    if (x_out && (e = gym_unpack_lanes(b->x[0], b->x[1], b->res_buf, x_out, b->B, b->Bp, b->N, 4, 2, s))) return e;
-    if (u_out && (e = gym_unpack_lanes(b->u[0], b->u[1], b->res_buf, u_out, b->B, b->Bp, T, 2, 1, s))) return e;
-    if (K_out && (e = gym_unpack_gains(b->K1, K_out, b->B, b->Bp, T, s))) return e;
+    const int64_t* map = b->lane_map;   // results straight into the caller's lane order
+    if (x_out && (e = launch_unpack_tiled(SrcPairs{(const double2*)b->x[0], (const double2*)b->x[1], b->res_buf, 2},
+                                          x_out, b->B, b->Bp, b->N, 4, st, map)))
+        return e;
+    if (u_out && (e = launch_unpack_tiled(SrcPlanes{b->u[0], b->u[1], b->res_buf, 2}, u_out, b->B, b->Bp, T, 2, st,
+                                          map)))
+        return e;
+    if (K_out && (e = launch_unpack_tiled(SrcGains{(const double2*)b->K1}, K_out, b->B, b->Bp, T, 8, st, map)))
+        return e;
     if (sig_out && (e = gym_newton_sigma(m, w, b, sig_out, s))) return e;
     return 0;
 }
@@ -2004,7 +2013,7 @@ int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* 
         if (e) return e;
     }
     return launch_unpack_tiled(SrcSigma{kw(*w), b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter}, sig_out, b->B, b->Bp,
-                               T, 2, st);
+                               T, 2, st, b->lane_map);
 }
 
 static int sweep_grid(int64_t Bp, int G) {

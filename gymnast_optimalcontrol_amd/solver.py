@@ -304,15 +304,18 @@ class BatchedNewtonSolver:
         else:
             log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every,
                               log_every=log_every, keep_stats=keep_stats)
-        x, u, K, s = self.finalize()
         B = self.B
         if perm is None:
             back = slice(0, B)
-        else:   # internal lane i is input lane perm[i]: gather the input order back
+        else:   # internal lane i is input lane perm[i]: finalize writes row perm[i]; gather the scalars back
             back = torch.empty_like(perm)
             back[perm] = torch.arange(B, device=perm.device)
+            self.batch.lane_map = perm.data_ptr()
+        try:
+            x, u, K, s = self.finalize()
+        finally:
+            self.batch.lane_map = None
         lanes = lambda t: t[:B][back]  # noqa: E731
-        x, u, K, s = x[back], u[back], K[back], s[back]
         n_iter = lanes(self.n_iter)
         res = dict(cost=lanes(self.cost), status=lanes(self.status), n_rollouts=lanes(self.n_roll),
                    gamma=lanes(self.gamma),

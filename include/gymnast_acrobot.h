@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 5
+#define GYM_ABI_VERSION 6
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -129,6 +129,8 @@ typedef struct gym_batch {
     double* stats;      /* (24) [0,8) totals (see gym_newton_iteration), [8,16) H0, [16,24) H1 */
     double* hist_cost;  /* optional (hist_len, Bp): J after iteration k            */
     double* hist_smax;  /* optional (hist_len, Bp): max|sigma| of iteration k      */
+    const int64_t* lane_map; /* optional (B): lane i's results go to row lane_map[i] of the lane-major outputs
+                         * of gym_newton_finalize / gym_newton_sigma (a permutation; NULL: identity)  */
     gym_timing* timing; /* [host] optional kernel timing (NULL: none)               */
 } gym_batch;
 
