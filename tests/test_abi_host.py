@@ -169,3 +169,20 @@ def test_get_fully_actuated_ref(tmp_path, golden):
     np.testing.assert_array_equal(x_ref, g["x_ref"])
     np.testing.assert_array_equal(u_ref, g["u_ref"])
     np.testing.assert_array_equal(t, g["t_ref"])
+
+
+def test_morton_order_groups_nearby_initial_states():
+    """solve()'s lane order (solver.morton_order): a permutation of the lanes, robust to non-finite states, and
+    neighbouring initial states end up in the same 64-lane group more often than in input order."""
+    import torch
+    from gymnast_optimalcontrol_amd.solver import morton_order
+    rng = np.random.default_rng(0)
+    x0 = np.zeros((4096, 4)); x0[:, :2] = rng.uniform(-0.5, 0.5, (4096, 2))
+    x0[7] = np.nan; x0[9, 0] = np.inf
+    p = morton_order(torch.from_numpy(x0)).numpy()
+    assert np.array_equal(np.sort(p), np.arange(4096))
+    xs = np.nan_to_num(x0[p], nan=0.0, posinf=0.0, neginf=0.0)[:, :2].reshape(-1, 64, 2)
+    xr = np.nan_to_num(x0, nan=0.0, posinf=0.0, neginf=0.0)[:, :2].reshape(-1, 64, 2)
+    spread = lambda g: float(np.mean(g.max(1) - g.min(1)))   # noqa: E731  mean per-group extent
+    assert spread(xs) < 0.3 * spread(xr)
+    assert np.array_equal(morton_order(torch.zeros((5, 4), dtype=torch.float64)).numpy(), np.arange(5))   # ties: stable
