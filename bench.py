@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
                     help="solver schedule (auto: the solver's choice for the batch size)")
-    ap.add_argument("--chunk", type=int, default=0,
+    ap.add_argument("--chunk", type=int, default=128,
                     help="persistent schedule: iterations per launch (0: all of max_iters in one launch)")
     a = ap.parse_args()
     if a.batch is None:

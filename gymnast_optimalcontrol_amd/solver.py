@@ -87,7 +87,7 @@ class BatchedNewtonSolver:
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
-                 chunk: int = 0, reorder: bool = True):
+                 chunk: int = 128, reorder: bool = True):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         self.eng = engine
@@ -138,7 +138,10 @@ class BatchedNewtonSolver:
         if persistent is None:   # automatic only when the caller chose no schedule at all
             persistent = pipeline is None and self.B <= self.persistent_max_lanes(dev)
         self.persistent = bool(persistent) and not self.checkpoint
-        self.chunk = int(chunk)          # iterations per persistent launch (0: all of max_iters in one)
+        # iterations per persistent launch (0: all of max_iters in one).  128 keeps one launch to ~0.15 s at the
+        # batch sizes that use the schedule (a non-converging batch at max_iters = 5000 would otherwise hold the
+        # GPU in one multi-second kernel); the 3-4 launch boundaries of a headline solve cost nothing measurable.
+        self.chunk = int(chunk)
         # solve() works on the lanes in the Morton order of their initial states (see morton_order)
         self.reorder = bool(reorder)
         self.lane_order = None
@@ -351,7 +354,7 @@ def morton_order(x0: torch.Tensor, bits: int = 10) -> torch.Tensor:
 
 
 def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_every: int, keep_stats: bool):
-    """Persistent schedule: launches of ``chunk`` iterations (all of max_iters by default); after each one the
+    """Persistent schedule: launches of ``chunk`` iterations (0: all of max_iters); after each one the
     statistics are all-reduced across ranks (``reduce_stats``) and read, and the loop stops when no lane of any
     rank is active."""
     log = []
