@@ -1337,6 +1337,11 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
 #ifndef GYM_RUN_BAND
 #define GYM_RUN_BAND 0
 #endif
+// waves per SIMD the persistent kernel is compiled for: it serves batches of at most 96 lanes per CU, i.e. at
+// most one wavefront per SIMD, so its register budget need not leave room for more
+#ifndef GYM_RUN_WAVES
+#define GYM_RUN_WAVES 1
+#endif
 // Everything the kernel needs beyond the stage loops' own operands is one by-value struct whose fields are
 // re-read from the kernel-argument segment at each use (run_args(): scalar loads behind an opaque pointer),
 // so that none of its ~20 pointers is held in SGPRs across the stage loops (spilled, they cost v_readlane
@@ -1371,7 +1376,7 @@ __device__ __forceinline__ void lane_fence() {   // this lane's stores visible t
 }
 
 template <bool U0Z>
-__global__ __launch_bounds__(BLK, 4) void k_nt_run(RunArgs args) {
+__global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
     constexpr bool BAND = GYM_RUN_BAND == 1;
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= args.B) return;
