@@ -181,6 +181,7 @@ struct Jac {
 
 __device__ __forceinline__ Jac jacobian(const Dyn& m, double th1, double th2, double w1, double w2, double tau2,
                                         const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits (see Sweep::step_j)
     double s1, c1, s2, c2;
     fast_sincos(th1, &s1, &c1, k);
     fast_sincos(th2, &s2, &c2, k);

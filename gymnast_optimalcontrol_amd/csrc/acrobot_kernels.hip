@@ -350,8 +350,18 @@ struct Sweep {
                                          const double* xrt, const double* urt, double& k0, double& k1,
                                          double& k2, double& k3, double& s0, double& s1,
                                          const gym::PolyRegs& pk = gym::poly_lits()) {
+        step_j(m, w, gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1, pk), xa, xb, ut0, ut1, xrt, urt, k0, k1, k2, k3,
+               s0, s1);
+    }
+    // the same with the stage's Jacobian already evaluated (it depends on x_t, u_t only, not on P)
+    __device__ __forceinline__ void step_j(const Dyn& m, const KW& w, const gym::Jac& J, double2 xa, double2 xb,
+                                           double ut0, double ut1, const double* xrt, const double* urt, double& k0,
+                                           double& k1, double& k2, double& k3, double& s0, double& s1) {
+        // FMA contraction within each expression only, never across statements: the bits then do not depend on
+        // the context the stage is compiled into (the interleaved sweep of backward_solver_lane_ilp, the sigma1
+        // re-runs) -- with cross-statement fusion they did
+#pragma clang fp contract(on)
         const double dt = m.h;
-        const gym::Jac J = gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1, pk);
         // A_d rows 2,3 (rows 0,1 = [1 0 dt 0], [0 1 0 dt]); B_d = dt * [0 0 bc2 bc3]^T in column 1
         const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
         const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
@@ -464,6 +474,7 @@ __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int 
                                             double k0, double k1, double k2, double k3, double s1) {
     const auto rC = rsrc(Cb + (int64_t)t * row);
     if (OUT != OUT_SIGMA) {
+#pragma clang fp contract(on)
         const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         bst2(rK, o2, 0, k0, k1);
@@ -517,6 +528,71 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
         S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
         store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, xa, xb, ut1, g0, k0, k1, k2, k3, s1);
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// The solver sweep for ONE wavefront per SIMD (the persistent kernel at its batch sizes), where a stage's time is
+// its dependency chain, not the SIMD's issue rate: stage t-1's Jacobian (a function of x_{t-1}, u_{t-1} only) is
+// evaluated beside stage t's Riccati update, so the two chains interleave.  That needs stage t-1's streams in
+// registers one stage early: prefetch distance 2, three stream sets and two Jacobians in rotation (unrolled by
+// 6, so that no set is copied -- a copy of a loading register waits for its load).  Same per-stage arithmetic
+// as backward_solver_lane (step = jacobian + step_j): the same bits.
+struct SweepStage {
+    double2 xa, xb;
+    double u0, u1;
+};
+template <bool U0Z, int OUT>
+__device__ __forceinline__ void backward_solver_lane_ilp(const Dyn& m, const KW& w,
+                                                         const double2* __restrict__ x, const double* __restrict__ u,
+                                                         const double* __restrict__ xr, const double* __restrict__ ur,
+                                                         double2* __restrict__ K1, double* __restrict__ cs, double g0,
+                                                         int64_t l, int64_t Bp, int N, double& dJ_out,
+                                                         double& smax_out) {
+    const int T = N - 1;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Xb = reinterpret_cast<const char*>(x);
+    const char* Ub = reinterpret_cast<const char*>(u);
+    const char* Kb = reinterpret_cast<const char*>(K1);
+    const char* Cb = reinterpret_cast<const char*>(cs);
+    Sweep<false> S(w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    auto fetch = [&](SweepStage& q, int t) {
+        const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)t * row);
+        q.xa = bld2(rX, o2, 0);
+        q.xb = bld2(rX, o2, WROW);
+        q.u0 = U0Z ? 0.0 : bld1(rU, o1, 0);
+        q.u1 = bld1(rU, o1, plane);
+    };
+    auto jac = [&](const SweepStage& q) {
+        const KArgs ka = kernarg_consts();
+        return gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
+    };
+    // stage t: c = its streams, Jc = its Jacobian; n = stage t-1's streams (landed), f <- stage t-2's
+    auto stage = [&](const SweepStage& c, const SweepStage& n, SweepStage& f, const gym::Jac& Jc, gym::Jac& Jn,
+                     int t) {
+        if (t < 0) return;
+        if (t >= 2) fetch(f, t - 2);
+        if (t >= 1) Jn = jac(n);
+        double k0, k1, k2, k3, s0, s1;
+        const KArgs ka = kernarg_consts();
+        S.step_j(ka.m, ka.w, Jc, c.xa, c.xb, c.u0, c.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, c.xa, c.xb, c.u1, g0, k0, k1, k2, k3, s1);
+    };
+    SweepStage A, B, C;
+    gym::Jac J0, J1;
+    fetch(A, T - 1);
+    if (T >= 2) fetch(B, T - 2);
+    J0 = jac(A);
+    for (int t = T - 1; t >= 0; t -= 6) {
+        stage(A, B, C, J0, J1, t);
+        stage(B, C, A, J1, J0, t - 1);
+        stage(C, A, B, J0, J1, t - 2);
+        stage(A, B, C, J1, J0, t - 3);
+        stage(B, C, A, J0, J1, t - 4);
+        stage(C, A, B, J1, J0, t - 5);
     }
     dJ_out = S.dJ;
     smax_out = S.smax;
@@ -1342,6 +1418,10 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
 #ifndef GYM_RUN_WAVES
 #define GYM_RUN_WAVES 1
 #endif
+// the persistent kernel's sweep interleaves stage t-1's Jacobian with stage t's Riccati (backward_solver_lane_ilp)
+#ifndef GYM_RUN_ILP
+#define GYM_RUN_ILP 1
+#endif
 // Everything the kernel needs beyond the stage loops' own operands is one by-value struct whose fields are
 // re-read from the kernel-argument segment at each use (run_args(): scalar loads behind an opaque pointer),
 // so that none of its ~20 pointers is held in SGPRs across the stage loops (spilled, they cost v_readlane
@@ -1396,8 +1476,12 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
         {
             const rargs_t R = run_args();
             double d, s;
-            backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1, R->cs,
-                                                        R->a.gamma0, l, R->Bp, R->N, d, s);
+            if (GYM_RUN_ILP)
+                backward_solver_lane_ilp<U0Z, OUT_SOLVER>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1,
+                                                          R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
+            else
+                backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1,
+                                                            R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
             const rargs_t Q = run_args();
             Q->dJ[l] = d;
             Q->smax[l] = s;
