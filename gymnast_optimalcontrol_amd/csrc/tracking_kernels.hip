@@ -152,13 +152,12 @@ __global__ __launch_bounds__(64) void k_dare_fixed_point(const double* __restric
         const double apb0 = ((a[i] * sPB[0] + a[4 + i] * sPB[2]) + a[8 + i] * sPB[4]) + a[12 + i] * sPB[6];
         const double apb1 = ((a[i] * sPB[1] + a[4 + i] * sPB[3]) + a[8 + i] * sPB[5]) + a[12 + i] * sPB[7];
         const double nP = (Q.v[4 * i + j] + apa) + (apb0 * K0 + apb1 * K1);
-        double d = own ? fabs(nP - P) : 0.0;
-#pragma unroll
-        for (int off = 8; off > 0; off >>= 1) d = fmax(d, __shfl_xor(d, off, 64));
-        d = __shfl(d, 0, 64);
+        // np.max(np.abs(P_next - P)) < tol (:160-163) as a wave vote: every entry below tol (a NaN entry is not,
+        // as np.max would return NaN); no cross-lane data movement on the iteration's critical path
+        const bool conv = __all(!own || fabs(nP - P) < tol);
         P = nP;
         __syncthreads();   // every lane has read sP / sPA / sPB before the next iteration rewrites them
-        if (d < tol) { it = n + 1; break; }
+        if (conv) { it = n + 1; break; }
     }
     if (own) P_out[ln] = P;
     if (ln == 0) *iters = it;
@@ -212,6 +211,7 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
 #pragma unroll
     for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
     f[0] = u_ff[0]; f[1] = u_ff[1];
+    const gym::PolyRegs pk = gym::poly_vgprs();   // minimax coefficients held in VGPRs (acrobot_device.hpp)
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
         const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
             f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
         }
         ul[t] = make_double2(v0, v1);
-        gym::rk4(m, n0, n1, n2, n3, v1);
+        gym::rk4(m, n0, n1, n2, n3, v1, pk);
         xl[2 * (t + 1)] = make_double2(n0, n1);
         xl[2 * (t + 1) + 1] = make_double2(n2, n3);
     }
