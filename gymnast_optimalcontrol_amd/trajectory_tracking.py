@@ -40,6 +40,18 @@ def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy()
 
 
+_FINAL_STATE = {}
+
+
+def _final_state(eng):
+    """X_F, U_F (:31-32) as device tensors, made once per device: a pageable host-to-device copy inside every
+    mpc_gains call would make the host wait for the GPU and leave the GPU idle while Python enqueues the run."""
+    key = str(eng.device)
+    if key not in _FINAL_STATE:
+        _FINAL_STATE[key] = (eng.t(X_F.reshape(1, 4)), eng.t(U_F.reshape(1, 2)))
+    return _FINAL_STATE[key]
+
+
 def _discrete(eng, A_c, B_c):
     eye = torch.eye(4, dtype=A_c.dtype, device=A_c.device)
     return eye + eng.dt * A_c, eng.dt * B_c                      # trajectory_generation.py:161-164
@@ -103,7 +115,7 @@ def mpc_gains(x_ref, u_ref, T_pred: int = T_PRED, Q=Q_MPC, R=R_MPC, n_steps: int
     S = x_ref.shape[0] - 1                                          # A_list: one stage per u_ref row (:19)
     n_steps = S if n_steps is None else int(n_steps)
     A_c, B_c = eng.jacobians(x_ref[:S], u_ref[:S])
-    Af_c, Bf_c = eng.jacobians(X_F.reshape(1, 4), U_F.reshape(1, 2))
+    Af_c, Bf_c = eng.jacobians(*_final_state(eng))
     A_f, B_f = _discrete(eng, Af_c[0], Bf_c[0])
     QT, _ = eng.dare_fixed_point(A_f, B_f, Q, R)
     K0 = eng.tv_lqr_gains(A_c, B_c, Q, R, QT, L=int(T_pred), nwin=n_steps, all_gains=False,
