@@ -230,7 +230,9 @@ def main():
                   "lane0_iters": int(res.n_iter[0].item()), "tolerance": 1e-8,
                   "converged_frac": float((st == 1).mean()), "ls_failed": int((st == 2).sum()),
                   "outer_iterations": int(n_iters_outer),
-                  "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())]}
+                  "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())],
+                  "rollouts": int(res.n_rollouts.sum().item()),
+                  "lanes_that_backtracked": int((res.n_rollouts > res.n_iter).sum().item())}
 
     value = lane_its_all / elapsed
     out = {"metric": METRIC, "value": value, "unit": "Newton iterations/s", "n_gpus": world, "steps": a.steps,
@@ -275,12 +277,17 @@ def main():
                     kern[kind]["achieved_GBs"] = per_launch / (kern[kind]["avg_ms"] * 1e-3) / 1e9
             dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
             bytes_per_lane, unit_note = ab[dom], f"one {dom} pass of one lane"
-        traffic, traffic_ratio = None, None
+        traffic, traffic_ratio, valu = None, None, None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):      # committed rocprofv3 --pmc measurement (tools/profile.sh, parse_profiles.py)
             try:
                 t = json.load(open(tfile)).get(dom, {})
                 traffic, traffic_ratio = t.get("hbm_bytes_per_launch"), t.get("traffic_over_algorithmic")
+                if "valu_busy_upper_est" in t:
+                    valu = {"busy_upper_est": t["valu_busy_upper_est"],
+                            "wave_instructions_per_launch": t["sq_insts_valu_per_launch"],
+                            "note": "SQ_INSTS_VALU x 4 cycles (fp64 wave64 on SIMD-32) / SIMD-cycles of the launch, "
+                                    "rocprofv3 PMC (profiles/pmc_traffic.json)"}
             except Exception:
                 traffic = None
         ach = kern[dom]["achieved_GBs"]
@@ -291,7 +298,8 @@ def main():
                            "unit_of_work": unit_note, "algorithmic_bytes_per_launch":
                            kern[dom]["algorithmic_bytes_per_launch"], "u0_zero_streams_skipped": solver.u0_zero,
                            "survey_bytes_per_iteration": ab["survey_per_iteration"],
-                           "whole_solve_GBs_at_survey_bytes": value * ab["survey_per_iteration"] / 1e9 / world}
+                           "whole_solve_GBs_at_survey_bytes": value * ab["survey_per_iteration"] / 1e9 / world,
+                           "fp64_valu": valu}
         out["kernels"] = kern
         out["schedule"] = "persistent" if solver.persistent else ("pipelined" if solver.pipeline else "serial")
     if parity is not None:

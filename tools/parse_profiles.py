@@ -78,6 +78,15 @@ def main():
         if k in algo:
             v["algorithmic_bytes_per_launch"] = float(algo[k])
             v["traffic_over_algorithmic"] = v["hbm_bytes_per_launch"] / algo[k]
+    # fp64 VALU issue estimate: SQ_INSTS_VALU wave-instructions x 4 cycles (a wave64 fp64 FMA on a 32-wide SIMD;
+    # 32-bit VALU takes 2, so this is an upper estimate) over the SIMD-cycles of the launch; GRBM_GUI_ACTIVE is
+    # summed over the 8 XCDs (3.2e7 for a ~1.7 ms launch at 2.4 GHz), 1024 SIMDs in all
+    for k, d in pmc.items():
+        if k in traffic and "SQ_INSTS_VALU" in d and "GRBM_GUI_ACTIVE" in d:
+            valu, gui = d["SQ_INSTS_VALU"]["mean"], d["GRBM_GUI_ACTIVE"]["mean"]
+            traffic[k]["sq_insts_valu_per_launch"] = valu
+            traffic[k]["grbm_gui_active_per_launch"] = gui
+            traffic[k]["valu_busy_upper_est"] = valu * 4.0 / (1024.0 * gui / 8.0)
     # bench.py names the dominant kernel "phase" (pipelined) or "backward" / "trial" (serial)
     alias = {"k_nt_phase": "phase", "k_nt_backward": "backward", "k_nt_trial": "trial"}
     out = {alias.get(k, k): v for k, v in traffic.items()}
