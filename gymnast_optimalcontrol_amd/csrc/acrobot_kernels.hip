@@ -1063,29 +1063,45 @@ struct SrcSigma {   // sigma of each lane's last iteration: sigma0 recomputed fr
     }
 };
 
-// dst (B, L, C) lane-major; grid (Bp / 64) x ceil(L / TS); dynamic LDS TS * C * TILE_PITCH doubles
-template <class Src>
+// dst (B, L, C) lane-major; grid (Bp / 64) x ceil(L / TS); dynamic LDS TS * C * TILE_PITCH doubles.
+// CT: C at compile time (the solver's outputs: 2, 4, 8 -- the divisions by C become shifts and the stores 16 B
+// wide), 0 = C at run time (gym_unpack_lanes' general form).
+template <class Src, int CT>
 __global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* __restrict__ dst,
                                                                const int64_t* __restrict__ map, int64_t B,
-                                                               int64_t Bp, int L, int C, int TS) {
+                                                               int64_t Bp, int L, int C_rt, int TS) {
     extern __shared__ double tile[];
+    __shared__ int64_t rows_of[BLK];                        // output row of each lane of the group
+    const int C = CT ? CT : C_rt;
     const int64_t g0 = (int64_t)blockIdx.x * BLK;          // first lane of the group
     const int t0 = (int)blockIdx.y * TS;
     const int ts = (L - t0 < TS) ? L - t0 : TS;
     const int rows = ts * C;
+    if (threadIdx.x < BLK) {
+        const int64_t l = g0 + threadIdx.x;
+        rows_of[threadIdx.x] = map ? (l < B ? map[l] : 0) : l;
+    }
     for (int i = threadIdx.x; i < rows * BLK; i += TILE_THREADS) {
         const int ln = i & (BLK - 1), r = i >> 6;          // r = knot * C + component
         tile[r * TILE_PITCH + ln] = src(t0 + r / C, r % C, g0 + ln, Bp);
     }
     __syncthreads();
     const int64_t nl = (B - g0 < BLK) ? B - g0 : BLK;      // real lanes of the group
-    for (int i = threadIdx.x; i < nl * rows; i += TILE_THREADS) {
-        const int ln = i / rows, r = i - ln * rows;
-        const int64_t row = map ? map[g0 + ln] : g0 + ln;   // output lane (the caller's order)
-        dst[(row * L + t0) * C + r] = tile[r * TILE_PITCH + ln];
+    if (CT > 0 && CT % 2 == 0) {   // component pairs: 16-byte stores
+        const int half = rows / 2;
+        double2* d2 = reinterpret_cast<double2*>(dst);
+        for (int i = threadIdx.x; i < nl * half; i += TILE_THREADS) {
+            const int ln = i / half, r2 = i - ln * half;
+            d2[((rows_of[ln] * L + t0) * C) / 2 + r2] =
+                make_double2(tile[(2 * r2) * TILE_PITCH + ln], tile[(2 * r2 + 1) * TILE_PITCH + ln]);
+        }
+    } else {
+        for (int i = threadIdx.x; i < nl * rows; i += TILE_THREADS) {
+            const int ln = i / rows, r = i - ln * rows;
+            dst[(rows_of[ln] * L + t0) * C + r] = tile[r * TILE_PITCH + ln];
+        }
     }
 }
-
 
 // ------------------------------------------------------------------------------------------
 // kernels: batched Newton / Armijo solver (newton_Algorithm :298-398)
@@ -1752,8 +1768,15 @@ int launch_unpack_tiled(const Src& src, double* dst, int64_t B, int64_t Bp, int 
     const int ts = tile_knots(C);
     if (C * TILE_PITCH > TILE_DOUBLES) return GYM_EINVAL;
     const dim3 grid((unsigned)(Bp / BLK), (unsigned)((L + ts - 1) / ts));
-    hipLaunchKernelGGL(k_unpack_tiled<Src>, grid, dim3(TILE_THREADS), sizeof(double) * ts * C * TILE_PITCH, st, src,
-                       dst, map, B, Bp, L, C, ts);
+    const size_t lds = sizeof(double) * ts * C * TILE_PITCH;
+    if (C == 2)
+        hipLaunchKernelGGL((k_unpack_tiled<Src, 2>), grid, dim3(TILE_THREADS), lds, st, src, dst, map, B, Bp, L, C, ts);
+    else if (C == 4)
+        hipLaunchKernelGGL((k_unpack_tiled<Src, 4>), grid, dim3(TILE_THREADS), lds, st, src, dst, map, B, Bp, L, C, ts);
+    else if (C == 8)
+        hipLaunchKernelGGL((k_unpack_tiled<Src, 8>), grid, dim3(TILE_THREADS), lds, st, src, dst, map, B, Bp, L, C, ts);
+    else
+        hipLaunchKernelGGL((k_unpack_tiled<Src, 0>), grid, dim3(TILE_THREADS), lds, st, src, dst, map, B, Bp, L, C, ts);
     return launch_status();
 }
 
