@@ -482,3 +482,23 @@ def test_state_checkpointing_is_bitwise_identical(task2_refs, pipeline, u0z, N):
         a, b = getattr(rc, name).cpu().numpy(), getattr(rf, name).cpu().numpy()
         assert np.array_equal(a, b, equal_nan=True), name
     assert np.array_equal(np.asarray(rc.stats_log), np.asarray(rf.stats_log), equal_nan=True)
+
+
+@pytest.mark.parametrize("C,W", [(1, 1), (2, 2), (2, 1), (3, 1), (4, 2), (6, 2), (8, 2), (8, 1), (12, 2), (13, 1)])
+def test_lane_transposes_round_trip(eng, C, W):
+    """gym_pack_lanes -> gym_unpack_lanes is the identity, bitwise, on a ragged batch over several LDS tiles of
+    knots: the compile-time component counts of the tiled unpack (2, 4, 8) and its run-time form, pairs and planes,
+    and the per-lane src0 / src1 select."""
+    import torch
+    B, L = 200, 501
+    Bp = (B + 63) // 64 * 64
+    g = torch.Generator().manual_seed(10 * C + W)
+    a = torch.randn(B, L, C, generator=g, dtype=torch.float64)
+    b = torch.randn(B, L, C, generator=g, dtype=torch.float64)
+    sa, sb = eng.pack(a.to(eng.device), Bp, W), eng.pack(b.to(eng.device), Bp, W)
+    if W == 1:
+        assert not sa[:, :, B:, :].any()          # padding lanes are zero-filled
+    assert torch.equal(eng.unpack(sa, B).cpu(), a)
+    sel = (torch.arange(B) % 3 == 1).to(torch.int32)
+    got = eng.unpack(sa, B, sb, sel.to(eng.device)).cpu()
+    assert torch.equal(got, torch.where(sel.bool()[:, None, None], b, a))
