@@ -238,7 +238,7 @@ def main():
     out = {"metric": METRIC, "value": value, "unit": "Newton iterations/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": f"cfg3: {a.batch} randomised-theta0 acrobot swing-ups per GPU, T={T}, fp64, "
+           "config": {"workload": f"{ {4096: 'cfg2', 262144: 'cfg3'}.get(a.batch, 'custom') }: {a.batch} randomised-theta0 acrobot swing-ups per GPU, T={T}, fp64, "
                                   "task-2 Newton/Armijo settings, solved to convergence",
                       "lanes_per_gpu": a.batch, "global_lanes": total, "horizon_T": T,
                       "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats / iteration)"},
