@@ -10,10 +10,13 @@ tol 1e-4, gamma_0 0.1, beta 0.7, c 0.5, <= 20 Armijo trials, max_iters 5000) of 
 of synthetic lanes, from u = 0 to every lane converged / failed, with inputs resident in HBM.
 Workload (N=1): BASELINE cfg 3 -- 262,144 lanes per GPU, x0 = [th1, th2, 0, 0], th ~ U(-0.5,0.5)
 (numpy default_rng(0)), lane 0 = 0 (the golden lane), T = 500 stages, fp64.  Weak scaling: every GPU
-owns 262,144 lanes; ranks exchange one 64-byte all-reduce per outer iteration.
+owns 262,144 lanes; ranks exchange one 64-byte all-reduce per host sync of the statistics.
 
 value = lane-iterations executed by all ranks / max-over-ranks wall time  ("Newton iterations/s";
-states/s = value * T).  Prints ONE JSON line on rank 0.
+states/s = value * T).  Prints ONE JSON line on rank 0.  Secondary legs timed in the same process and
+reported inside that line (--extra-legs): "strong_scaling_cfg4" (BASELINE cfg 4: 1,048,576 lanes
+strong-scaled over the N ranks) and, at N = 1, "general_path" (the same workload on the general kernels that
+stream the tau1 planes).  --workload cfg4 makes cfg 4 the main line; --workload mpc runs BASELINE cfg 5.
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "swing-up Newton iterations/sec (batch×T states/s) at 1/2/4/8 MI355X"
+CFG4_LANES = 1048576           # BASELINE cfg 4: global lanes sharded over 8 GPUs
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
 
@@ -82,6 +86,21 @@ def cpu_baseline(x0, x_ref, u_ref, lanes: int, max_iters: int):
             "sample": f"first {lanes} lanes of the bench workload solved to convergence ({its} lane-iterations, "
                       f"{dt:.1f} s) by oracle/acrobot_oracle.c (fp64, OpenMP {threads} threads)",
             "seconds": dt, "lane_iterations": its}
+
+
+def numpy_baseline(x0, x_ref, u_ref, lanes: int, iters: int):
+    """The NumPy restatement (oracle/acrobot_np.py: the reference's dense algorithm vectorised over lanes) on a
+    bounded sample: the first ``lanes`` lanes, ``iters`` Newton iterations from u = 0."""
+    from oracle import acrobot_np as an
+    an._model(1)                                   # sympy model build: setup, not timed
+    t0 = time.perf_counter()
+    r = an.newton_solve(x0[:lanes], x_ref, u_ref, iters, tol=1e-4, gamma_0=0.1)
+    dt = time.perf_counter() - t0
+    its = int(np.asarray(r["n_iter"]).sum())
+    return {"value": its / dt, "unit": "Newton iterations/s", "cores": 1, "kind": "port",
+            "sample": f"first {lanes} lanes of the bench workload, {iters} Newton iterations from u = 0 "
+                      f"({its} lane-iterations, {dt:.1f} s), oracle/acrobot_np.py (numpy, lanes vectorised, "
+                      f"one Python thread)", "seconds": dt, "lane_iterations": its}
 
 
 def run_mpc(a):
@@ -148,108 +167,62 @@ def run_mpc(a):
     print(json.dumps(out), flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=None,
-                    help="lanes per GPU (weak scaling); default 262144 (newton, cfg 3) or 8192 (mpc, cfg 5)")
-    ap.add_argument("--max-iters", type=int, default=5000)
-    ap.add_argument("--cpu-lanes", type=int, default=4096,
-                    help="lanes of the bounded CPU-baseline sample (about 10 s on 16 host cores)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
-    ap.add_argument("--sync-every", type=int, default=4,
-                    help="outer iterations between host reads of the (all-reduced) statistics; iterations "
-                         "enqueued after every lane has finished are no-ops")
-    ap.add_argument("--workload", choices=("newton", "mpc"), default="newton",
-                    help="newton: the north-star metric (cfg 3); mpc: BASELINE cfg 5")
-    ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
-    ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
-                    help="solver schedule (auto: the solver's choice for the batch size)")
-    ap.add_argument("--chunk", type=int, default=128,
-                    help="persistent schedule: iterations per launch (0: all of max_iters in one launch)")
-    a = ap.parse_args()
-    if a.batch is None:
-        a.batch = 8192 if a.workload == "mpc" else 262144
-    if a.workload == "mpc":
-        return run_mpc(a)
+class NewtonLeg:
+    """One timed configuration of the batched solver on this rank: ``total`` global lanes of the bench workload,
+    this rank's contiguous shard, the schedule chosen on the largest shard (identical on every rank)."""
 
-    import torch
-    from gymnast_optimalcontrol_amd import distributed as gd
-    rank, local_rank, world = gd.init_process_group()
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(gd.local_device_index(local_rank))
-    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
-    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None):
+        from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+        self.rank, self.world = gd.rank_world()
+        self.total = int(total)
+        self.x0_all = make_x0(self.total)
+        lo, hi = gd.shard_range(self.total, self.rank, self.world)
+        sched = {"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule]
+        self.solver = BatchedNewtonSolver(
+            eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
+            persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
+            schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero)
+        if timing:
+            self.solver.enable_timing()
+        self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
+        self.reduce = gd.make_reduce_stats()
+        self.a, self.gd = a, gd
 
-    x_ref, u_ref = load_refs()
-    N = x_ref.shape[0]
-    T = N - 1
-    total = a.batch * world
-    x0_all = make_x0(total)
-    lo, hi = gd.shard_range(total, rank, world)
-    eng = AcrobotEngine()
-    solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20,
-                                 pipeline={"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule],
-                                 persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk)
-    if not a.no_timing:
-        solver.enable_timing()
-    x0_dev = eng.t(x0_all[lo:hi])                  # inputs resident in HBM before the timed region
-    reduce = gd.make_reduce_stats()
+    def run(self, steps: int, warmup: int):
+        import torch
+        a, gd, solver = self.a, self.gd, self.solver
+        for _ in range(warmup):
+            solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
+        solver.reset_timing()
+        gd.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lane_its, res = 0, None
+        for _ in range(steps):
+            res = None                                   # free the previous solve's outputs first
+            res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
+            lane_its += res.lane_iterations
+        torch.cuda.synchronize()
+        gd.barrier()
+        elapsed = gd.max_over_ranks(time.perf_counter() - t0)
+        self.res, self.lane_its, self.steps = res, lane_its, steps
+        self.elapsed = elapsed
+        self.lane_its_all = int(gd.sum_over_ranks(lane_its))
+        self.value = self.lane_its_all / elapsed
+        return self
 
-    for _ in range(a.warmup):
-        solver.solve(x0_dev, a.max_iters, reduce_stats=reduce, sync_every=a.sync_every)
-    solver.reset_timing()
-    gd.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    lane_its = 0
-    res = None
-    for _ in range(a.steps):
-        res = solver.solve(x0_dev, a.max_iters, reduce_stats=reduce, sync_every=a.sync_every)
-        lane_its += res.lane_iterations
-    torch.cuda.synchronize()
-    gd.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = gd.max_over_ranks(elapsed)
-    lane_its_all = int(gd.sum_over_ranks(lane_its))
-    kt = solver.kernel_times()
-    n_iters_outer = res.iterations
-
-    # parity of the golden lane (rank 0 owns lane 0)
-    parity = None
-    if rank == 0:
-        g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))
-        x0l, u0l = res.x[0].cpu().numpy(), res.u[0].cpu().numpy()
-        st = res.status.cpu().numpy()
-        parity = {"lane0_rel_l2_x": float(np.linalg.norm(x0l - g["x"]) / np.linalg.norm(g["x"])),
-                  "lane0_rel_l2_u": float(np.linalg.norm(u0l - g["u"]) / np.linalg.norm(g["u"])),
-                  "lane0_iters": int(res.n_iter[0].item()), "tolerance": 1e-8,
-                  "converged_frac": float((st == 1).mean()), "ls_failed": int((st == 2).sum()),
-                  "outer_iterations": int(n_iters_outer),
-                  "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())],
-                  "rollouts": int(res.n_rollouts.sum().item()),
-                  "lanes_that_backtracked": int((res.n_rollouts > res.n_iter).sum().item())}
-
-    value = lane_its_all / elapsed
-    out = {"metric": METRIC, "value": value, "unit": "Newton iterations/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": f"{ {4096: 'cfg2', 262144: 'cfg3'}.get(a.batch, 'custom') }: {a.batch} randomised-theta0 acrobot swing-ups per GPU, T={T}, fp64, "
-                                  "task-2 Newton/Armijo settings, solved to convergence",
-                      "lanes_per_gpu": a.batch, "global_lanes": total, "horizon_T": T,
-                      "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats / iteration)"},
-           "states_per_s": value * T}
-
-    if kt and rank == 0:
+    def kernel_report(self, N: int):
+        """Per-kernel HIP-event times (this rank) and the dominant kernel's algorithmic GB/s."""
+        solver = self.solver
+        kt = solver.kernel_times()
+        if not kt:
+            return None, None
         ab = algorithmic_bytes(N, solver.u0_zero)
         kern = {}
         for kind, (ms, launches) in kt.items():
             if launches:
                 kern[kind] = {"avg_ms": ms / launches, "launches": launches}
+        lane_its = self.lane_its
         if "run" in kern:
             # persistent schedule: every lane-iteration (sweep + trial) runs inside the run launches
             dom = "run"
@@ -263,7 +236,7 @@ def main():
             dom = "phase"
             rec_ms = sum(kern[k]["avg_ms"] * kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
             rec_n = sum(kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
-            total_launches = a.steps * (2 * n_iters_outer + 1)
+            total_launches = self.steps * (2 * self.res.iterations + 1)
             per_launch = lane_its * ab["iteration"] / total_launches
             kern["phase"] = {"avg_ms": rec_ms / rec_n, "launches": total_launches, "recorded": rec_n,
                              "algorithmic_bytes_per_launch": per_launch}
@@ -277,35 +250,182 @@ def main():
                     kern[kind]["achieved_GBs"] = per_launch / (kern[kind]["avg_ms"] * 1e-3) / 1e9
             dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
             bytes_per_lane, unit_note = ab[dom], f"one {dom} pass of one lane"
-        traffic, traffic_ratio, valu = None, None, None
-        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):      # committed rocprofv3 --pmc measurement (tools/profile.sh, parse_profiles.py)
-            try:
-                t = json.load(open(tfile)).get(dom, {})
-                traffic, traffic_ratio = t.get("hbm_bytes_per_launch"), t.get("traffic_over_algorithmic")
-                if "valu_busy_upper_est" in t:
-                    valu = {"busy_upper_est": t["valu_busy_upper_est"],
-                            "wave_instructions_per_launch": t["sq_insts_valu_per_launch"],
-                            "note": "SQ_INSTS_VALU x 4 cycles (fp64 wave64 on SIMD-32) / SIMD-cycles of the launch, "
-                                    "rocprofv3 PMC (profiles/pmc_traffic.json)"}
-            except Exception:
-                traffic = None
         ach = kern[dom]["achieved_GBs"]
-        out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
-                           "traffic_source": "profiles/pmc_traffic.json (rocprofv3 PMC, 20-iteration run, all lanes "
-                                             "active)", "bytes_per_unit": bytes_per_lane,
-                           "unit_of_work": unit_note, "algorithmic_bytes_per_launch":
-                           kern[dom]["algorithmic_bytes_per_launch"], "u0_zero_streams_skipped": solver.u0_zero,
-                           "survey_bytes_per_iteration": ab["survey_per_iteration"],
-                           "whole_solve_GBs_at_survey_bytes": value * ab["survey_per_iteration"] / 1e9 / world,
-                           "fp64_valu": valu}
+        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "bytes_per_unit": bytes_per_lane, "unit_of_work": unit_note,
+                "algorithmic_bytes_per_launch": kern[dom]["algorithmic_bytes_per_launch"],
+                "u0_zero_streams_skipped": solver.u0_zero}
+        return kern, roof
+
+    def schedule(self) -> str:
+        s = self.solver
+        return "persistent" if s.persistent else ("pipelined" if s.pipeline else "serial")
+
+    def free(self):
+        import torch
+        self.solver = self.res = self.x0_dev = None
+        torch.cuda.empty_cache()
+
+
+def pmc_traffic(dom: str):
+    """The committed rocprofv3 PMC measurement of the dominant kernel (tools/profile.sh, parse_profiles.py)."""
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    traffic, ratio, valu, src = None, None, None, None
+    if os.path.exists(tfile):
+        try:
+            d = json.load(open(tfile))
+            t = d.get(dom, {})
+            traffic, ratio = t.get("hbm_bytes_per_launch"), t.get("traffic_over_algorithmic")
+            src = d.get("source", "profiles/pmc_traffic.json (rocprofv3 PMC)")
+            if "valu_busy_upper_est" in t:
+                valu = {"busy_upper_est": t["valu_busy_upper_est"],
+                        "wave_instructions_per_launch": t["sq_insts_valu_per_launch"],
+                        "note": "SQ_INSTS_VALU x 4 cycles (fp64 wave64 on SIMD-32) / SIMD-cycles of the launch, "
+                                "rocprofv3 PMC (profiles/pmc_traffic.json)"}
+        except Exception:
+            traffic = None
+    return traffic, ratio, valu, src
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="lanes per GPU (weak scaling); default 262144 (newton, cfg 3) or 8192 (mpc, cfg 5)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many lanes in total, sharded over the ranks (cfg4: 1048576)")
+    ap.add_argument("--max-iters", type=int, default=5000)
+    ap.add_argument("--cpu-lanes", type=int, default=4096,
+                    help="lanes of the bounded C-oracle CPU-baseline sample (about 10 s on 16 host cores)")
+    ap.add_argument("--numpy-lanes", type=int, default=256,
+                    help="lanes of the bounded NumPy-restatement CPU-baseline sample (numpy-iters iterations)")
+    ap.add_argument("--numpy-iters", type=int, default=10)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--sync-every", type=int, default=4,
+                    help="outer iterations between host reads of the (all-reduced) statistics; iterations "
+                         "enqueued after every lane has finished are no-ops")
+    ap.add_argument("--workload", choices=("newton", "cfg4", "mpc"), default="newton",
+                    help="newton: the north-star metric (cfg 3 per GPU, weak scaling); cfg4: 1,048,576 lanes "
+                         "strong-scaled over the ranks; mpc: BASELINE cfg 5")
+    ap.add_argument("--extra-legs", default="cfg4,general",
+                    help="comma list of secondary timed legs reported inside the same JSON line (newton "
+                         "workload): cfg4 = 1,048,576 lanes strong-scaled over the ranks; general = the same "
+                         "workload on the general (tau1-streaming) kernels, N=1 only; '' for none")
+    ap.add_argument("--extra-steps", type=int, default=2, help="timed solves of each extra leg (1 warmup)")
+    ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
+    ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
+                    help="solver schedule (auto: the solver's choice for the batch size)")
+    ap.add_argument("--chunk", type=int, default=128,
+                    help="persistent schedule: iterations per launch (0: all of max_iters in one)")
+    ap.add_argument("--u0-zero", choices=("auto", "off"), default="auto",
+                    help="off: force the general kernels (tau1 planes streamed) for the main leg")
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 8192 if a.workload == "mpc" else 262144
+    if a.workload == "mpc":
+        return run_mpc(a)
+    if a.workload == "cfg4" and a.global_batch is None:
+        a.global_batch = CFG4_LANES
+
+    import torch
+    from gymnast_optimalcontrol_amd import distributed as gd
+    rank, local_rank, world = gd.init_process_group()
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(gd.local_device_index(local_rank))
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+
+    x_ref, u_ref = load_refs()
+    N = x_ref.shape[0]
+    T = N - 1
+    strong = a.global_batch is not None
+    total = a.global_batch if strong else a.batch * world
+    eng = AcrobotEngine()
+    main_leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing,
+                         u0_zero=False if a.u0_zero == "off" else None).run(a.steps, a.warmup)
+    res = main_leg.res
+    value = main_leg.value
+
+    # parity of the golden lane (rank 0 owns lane 0)
+    parity = None
+    if rank == 0:
+        g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))
+        x0l, u0l = res.x[0].cpu().numpy(), res.u[0].cpu().numpy()
+        st = res.status.cpu().numpy()
+        parity = {"lane0_rel_l2_x": float(np.linalg.norm(x0l - g["x"]) / np.linalg.norm(g["x"])),
+                  "lane0_rel_l2_u": float(np.linalg.norm(u0l - g["u"]) / np.linalg.norm(g["u"])),
+                  "lane0_iters": int(res.n_iter[0].item()), "tolerance": 1e-8,
+                  "converged_frac": float((st == 1).mean()), "ls_failed": int((st == 2).sum()),
+                  "outer_iterations": int(res.iterations),
+                  "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())],
+                  "rollouts": int(res.n_rollouts.sum().item()),
+                  "lanes_that_backtracked": int((res.n_rollouts > res.n_iter).sum().item())}
+
+    per_gpu = -(-total // world)
+    if strong:
+        label = (f"{'cfg4' if total == CFG4_LANES else 'custom'}: {total} randomised-theta0 acrobot swing-ups "
+                 f"strong-scaled over {world} GPU(s) ({per_gpu} per GPU)")
+    else:
+        label = (f"{ {4096: 'cfg2', 262144: 'cfg3'}.get(a.batch, 'custom') }: {a.batch} randomised-theta0 acrobot "
+                 f"swing-ups per GPU" + (f" x {world} GPUs (weak scaling)" if world > 1 else ""))
+    out = {"metric": METRIC, "value": value, "unit": "Newton iterations/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": 1e3 * main_leg.elapsed / a.steps, "higher_is_better": True,
+           "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": label + f", T={T}, fp64, task-2 Newton/Armijo settings, solved to convergence",
+                      "lanes_per_gpu": per_gpu, "global_lanes": total, "horizon_T": T,
+                      "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats per host sync)"},
+           "states_per_s": value * T}
+
+    kern, roof = main_leg.kernel_report(N)
+    if kern and rank == 0:
+        traffic, ratio, valu, src = pmc_traffic(roof["kernel"])
+        roof.update({"traffic": traffic, "traffic_over_algorithmic": ratio, "traffic_source": src,
+                     "survey_bytes_per_iteration": algorithmic_bytes(N)["survey_per_iteration"], "fp64_valu": valu})
+        # the ordering the contract prescribes: bound, achieved, peak, unit, frac, traffic first
+        out["roofline"] = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")}
+        out["roofline"].update({k: v for k, v in roof.items() if k not in out["roofline"]})
         out["kernels"] = kern
-        out["schedule"] = "persistent" if solver.persistent else ("pipelined" if solver.pipeline else "serial")
+    out["schedule"] = main_leg.schedule()
     if parity is not None:
         out["parity"] = parity
+    res = None
+    main_leg.free()
+
+    # secondary legs (same process, same JSON line)
+    legs = [s for s in a.extra_legs.split(",") if s] if a.workload == "newton" else []
+    if "cfg4" in legs and not strong:
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG4_LANES, not a.no_timing).run(a.extra_steps, 1)
+        k4, r4 = leg.kernel_report(N)
+        out["strong_scaling_cfg4"] = {
+            "value": leg.value, "unit": "Newton iterations/s", "scaling": "strong", "global_lanes": CFG4_LANES,
+            "lanes_per_gpu": -(-CFG4_LANES // world), "n_gpus": world, "steps": a.extra_steps, "warmup": 1,
+            "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
+            "roofline_frac": None if r4 is None else r4["frac"],
+            "note": "BASELINE cfg 4: 1,048,576 lanes sharded over the ranks (one all-reduce of 8 fp64 stats per "
+                    "host sync); max-over-ranks wall time"}
+        leg.free()
+    if "general" in legs and world == 1 and a.u0_zero == "auto":
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, u0_zero=False).run(a.extra_steps, 1)
+        kg, rg = leg.kernel_report(N)
+        out["general_path"] = {
+            "value": leg.value, "unit": "Newton iterations/s", "steps": a.extra_steps, "warmup": 1,
+            "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "roofline": None if rg is None else {k: rg[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
+                                                                     "bytes_per_unit")},
+            "specialisation_share": 1.0 - leg.value / value,
+            "note": "the same workload on the general kernels (u0_zero off: the tau1 planes are read and written, "
+                    "as for any reference with a live tau1 channel such as task 1); bitwise-identical results "
+                    "(tests/test_gpu_parity.py::test_u0_zero_stream_skipping_is_bitwise_identical)"}
+        leg.free()
+
     if rank == 0 and world == 1 and not a.no_cpu:
+        x0_all = make_x0(total)
         out["cpu_baseline"] = cpu_baseline(x0_all, x_ref, u_ref, a.cpu_lanes, a.max_iters)
+        out["cpu_baseline"]["numpy"] = numpy_baseline(x0_all, x_ref, u_ref, a.numpy_lanes, a.numpy_iters)
         out["cpu_baseline"]["reference_python_single_core"] = {
             "value": 5.0, "unit": "Newton iterations/s", "note": "reference newton_Algorithm, 1 core, build "
             "container (Intel Xeon), SURVEY.md 3.1: 0.199 s/iteration; not a same-box measurement"}

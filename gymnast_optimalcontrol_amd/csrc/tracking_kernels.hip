@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64) void k_dare_fixed_point(const double* __restric
 #pragma unroll
     for (int k = 0; k < 8; ++k) b[k] = Bm[k];
     double P = Q.v[4 * i + j];
-    int it = max_iter;
+    int it = max_iter + 1;                 // max_iter + 1: the tolerance was never met
     for (int n = 0; n < max_iter; ++n) {
         if (own) sP[ln] = P;
         __syncthreads();

@@ -30,6 +30,13 @@ def env_rank_world() -> tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def rank_world(group=None) -> tuple[int, int]:
+    """(rank, world_size) of the initialised process group, or (0, 1) for a single process."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
 def local_device_index(local_rank: int) -> int:
     """This rank's GPU: local_rank, wrapped onto the visible devices (one process per GPU on a full node; a
     multi-rank rehearsal on fewer GPUs shares them)."""
@@ -95,16 +102,29 @@ def sum_over_ranks(value: float, group=None) -> float:
     return float(t.item())
 
 
-def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, **solver_kw):
+def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool = False, **solver_kw):
     """Solve this rank's contiguous shard of ``x0_all`` (B_total,4); stop on the GLOBAL active count.
 
-    Returns (lo, hi, SolveResult of the local shard)."""
+    Every rank must hold a non-empty shard (``len(x0_all) >= world``; checked on every rank before any
+    collective, so all of them raise together).  The automatic schedule is chosen on the largest shard
+    (``schedule_lanes``), so every rank runs the same schedule and issues its all-reduces at the same
+    iterations.  Returns (lo, hi, SolveResult of the local shard)."""
     from .engine import AcrobotEngine
     from .solver import BatchedNewtonSolver
     rank = dist.get_rank() if dist.is_initialized() else 0
     world = dist.get_world_size() if dist.is_initialized() else 1
-    lo, hi = shard_range(len(x0_all), rank, world)
+    total = len(x0_all)
+    lo, hi = shard_range(total, rank, world)
+    if total < world:
+        raise ValueError(f"{total} lanes cannot be sharded over {world} ranks (every rank needs one)")
     eng = engine or AcrobotEngine()
+    solver_kw.setdefault("schedule_lanes", schedule_lanes(total, world))
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **solver_kw)
-    res = solver.solve(np.asarray(x0_all)[lo:hi], max_iters, reduce_stats=make_reduce_stats())
+    res = solver.solve(np.asarray(x0_all)[lo:hi], max_iters, reduce_stats=make_reduce_stats(), keep_stats=keep_stats)
     return lo, hi, res
+
+
+def schedule_lanes(total: int, world: int) -> int:
+    """The lane count every rank bases its automatic schedule choice on: the largest shard, identical on all
+    ranks (ragged shards differ by one lane and could otherwise straddle a schedule threshold)."""
+    return -(-int(total) // int(world))

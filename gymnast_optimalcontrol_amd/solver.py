@@ -58,6 +58,9 @@ class SolveResult:
     stats_log: list = field(default_factory=list)
     hist_cost: torch.Tensor | None = None   # (hist_len, B)
     hist_smax: torch.Tensor | None = None   # (hist_len, B)
+    x_trajs: dict | None = None             # {lane: [x_0, x_1, ...]} of the captured lanes (capture_lanes)
+    cost0: dict | None = None               # {lane: J_0} of the captured lanes
+    schedule: str = ""                      # "serial" | "pipelined" | "persistent"
 
 
 class BatchedNewtonSolver:
@@ -87,9 +90,14 @@ class BatchedNewtonSolver:
     def __init__(self, engine: AcrobotEngine, x_ref, u_ref, B: int, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
-                 chunk: int = 128, reorder: bool = True):
+                 chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
+                 capture_lanes=None, capture_every: int = 1):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
+        # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
+        # the largest shard of the global batch, so that every rank picks the same schedule: the schedules
+        # synchronise (all-reduce) at different points, and mixed choices would pair up the wrong collectives.
+        sched_B = self.B_sched = int(schedule_lanes) if schedule_lanes is not None else int(B)
         self.eng = engine
         self.x_ref, self.u_ref = engine.refs(x_ref, u_ref)
         self.B, self.Bp = int(B), padded(int(B))
@@ -114,7 +122,7 @@ class BatchedNewtonSolver:
         self.cand_ok = torch.zeros((max(int(max_ls), 1), Bp), dtype=torch.uint8, device=dev)
         self.partials = e(256 * 8)
         self.stats = torch.zeros(24, dtype=F64, device=dev)     # [0,8) totals, [8,16) / [16,24) halves
-        self.pipeline = (self.B >= self.pipeline_min_lanes(dev)) if pipeline is None else bool(pipeline)
+        self.pipeline = (sched_B >= self.pipeline_min_lanes(dev)) if pipeline is None else bool(pipeline)
         self.max_iters = None
         self.hist_len = int(hist_len)
         self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
@@ -136,7 +144,7 @@ class BatchedNewtonSolver:
         if persistent and self.checkpoint:
             raise ValueError("the persistent schedule does not support state checkpointing")
         if persistent is None:   # automatic only when the caller chose no schedule at all
-            persistent = pipeline is None and self.B <= self.persistent_max_lanes(dev)
+            persistent = pipeline is None and sched_B <= self.persistent_max_lanes(dev)
         self.persistent = bool(persistent) and not self.checkpoint
         # iterations per persistent launch (0: all of max_iters in one).  128 keeps one launch to ~0.15 s at the
         # batch sizes that use the schedule (a non-converging batch at max_iters = 5000 would otherwise hold the
@@ -157,6 +165,23 @@ class BatchedNewtonSolver:
         self.batch = b
         self.k = 0
         self.timing = None
+        # selected-lane trajectory capture (the reference's history['x_trajs'], trajectory_generation.py:322-327,
+        # 387-388): after every iteration the captured lanes' current iterates are gathered on the device; the
+        # persistent schedule then runs one iteration per launch.  Not combined with checkpointing (the state
+        # buffers hold checkpoints only).
+        self.capture_lanes = None if capture_lanes is None else [int(i) for i in capture_lanes]
+        if self.capture_lanes is not None:
+            if self.checkpoint:
+                raise ValueError("trajectory capture needs the full state store (checkpoint=False)")
+            if any(not (0 <= i < self.B) for i in self.capture_lanes):
+                raise ValueError(f"capture_lanes must lie in [0, {self.B})")
+        self.capture_every = max(int(capture_every), 1)
+        self._cap_pos = None
+        self._cap_log = []
+
+    @property
+    def schedule(self) -> str:
+        return "persistent" if self.persistent else ("pipelined" if self.pipeline else "serial")
 
     # --- optional per-kernel HIP-event timing (on the solver's stream) ---------------------
     def enable_timing(self):
@@ -203,6 +228,7 @@ class BatchedNewtonSolver:
         _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
+        self._capture_start(self.capture_lanes or [])
         if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
 
@@ -230,7 +256,55 @@ class BatchedNewtonSolver:
                                                          C.byref(self.armijo), C.byref(self.batch), k,
                                                          self.eng.stream), "gym_newton_iteration")
         self.k += 1
+        self._capture()
         return self.stats[:8]
+
+    # --- selected-lane trajectory capture -----------------------------------------------------
+    def _capture_start(self, positions):
+        """Begin capturing the lanes at internal positions ``positions`` (after init: the open-loop rollout)."""
+        self._cap_log = []
+        if self.capture_lanes is None:
+            self._cap_pos = None
+            return
+        self._cap_pos = torch.as_tensor(positions, dtype=torch.int64, device=self.eng.device)
+        self._capture(initial=True)
+
+    def _capture(self, initial: bool = False):
+        """Enqueue a gather of the captured lanes' current iterates (state buffer res_buf[lane]), their
+        iteration counts and statuses.  Device work only: no host synchronisation."""
+        if self._cap_pos is None or (not initial and self.k % self.capture_every):
+            return
+        pos = self._cap_pos
+        W = self.Bp // 64
+        # wave-blocked pairs: (N, Bp/64, 2 rows, 64 lanes, 2) -> (n_cap, N, 2, 2) per buffer (the advanced
+        # indices' dimension leads)
+        xs = [xb.view(self.N, W, 2, 64, 2)[:, pos // 64, :, pos % 64, :] for xb in self.x]
+        sel = self.res_buf[pos].to(torch.bool) if not initial else torch.zeros_like(pos, dtype=torch.bool)
+        x = torch.where(sel.view(-1, 1, 1, 1), xs[1], xs[0]).reshape(-1, self.N, 4)
+        self._cap_log.append((self.k, x.clone(), self.n_iter[pos].clone(), self.status[pos].clone(),
+                              self.cost[pos].clone()))
+
+    def captured_trajectories(self) -> dict:
+        """{caller lane: [x_0, x after each accepted iteration ...]} as (N,4) numpy arrays -- the reference's
+        history['x_trajs'] of each captured lane (entries only every ``capture_every`` iterations)."""
+        if self.capture_lanes is None:
+            return {}
+        out = {lane: [] for lane in self.capture_lanes}
+        for k, x, n_it, st, _ in self._cap_log:
+            x, n_it, st = x.cpu().numpy(), n_it.cpu().numpy(), st.cpu().numpy()
+            for j, lane in enumerate(self.capture_lanes):
+                if k == 0:
+                    out[lane].append(x[j])
+                elif n_it[j] == k and st[j] != _lib.LS_FAILED:   # the lane ran iteration k-1 and accepted it
+                    out[lane].append(x[j])
+        return out
+
+    def captured_initial_costs(self) -> dict:
+        """{caller lane: J_0} of the captured lanes (the reference's history['cost'][0])."""
+        if self.capture_lanes is None or not self._cap_log:
+            return {}
+        c0 = self._cap_log[0][4].cpu().numpy()
+        return {lane: float(c0[j]) for j, lane in enumerate(self.capture_lanes)}
 
     def finalize(self):
         B, N, T, dev = self.B, self.N, self.T, self.eng.device
@@ -302,6 +376,10 @@ class BatchedNewtonSolver:
             x0 = x0[perm]
         self.init(x0)
         self.lane_order = perm
+        if perm is not None and self.capture_lanes is not None:
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(self.B, device=perm.device)
+            self._capture_start(inv[torch.as_tensor(self.capture_lanes, device=perm.device)].tolist())
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:
@@ -328,6 +406,9 @@ class BatchedNewtonSolver:
         secs = time.perf_counter() - t0
         # persistent: the lanes' own iteration counts (no lock-step outer loop); otherwise the loop's count
         iters = int(n_iter.max().item()) if self.persistent else self.k
+        res["x_trajs"] = self.captured_trajectories() if self.capture_lanes is not None else None
+        res["cost0"] = self.captured_initial_costs() if self.capture_lanes is not None else None
+        res["schedule"] = self.schedule
         return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
                            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)
 
@@ -359,11 +440,17 @@ def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_ever
     rank is active."""
     log = []
     chunk = solver.chunk if solver.chunk > 0 else max(int(max_iters), 1)
+    # trajectory capture: one iteration per launch, but the statistics are still read (and all-reduced) at the
+    # same iterations as without capture, so ranks that capture and ranks that do not stay paired
+    step = 1 if solver._cap_pos is not None else chunk
     k = 0
     while k < max_iters:
-        k1 = min(int(max_iters), k + chunk)
+        k1 = min(int(max_iters), k + step)
         solver._run(k, k1)
         solver.k = k = k1
+        solver._capture()
+        if k % chunk and k < max_iters:
+            continue
         st = solver.stats[:8]
         if reduce_stats is not None:
             st = reduce_stats(st)
@@ -409,10 +496,11 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
 def newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
                        max_ls=MAX_LINE_SEARCH_ITERS, engine: AcrobotEngine | None = None, hist_len=0,
                        reduce_stats=None, pipeline: bool | None = None,
-                       persistent: bool | None = None) -> SolveResult:
+                       persistent: bool | None = None, capture_lanes=None) -> SolveResult:
     """Batched newton_Algorithm: x0 (B,4) -> SolveResult (device tensors)."""
     eng = engine or AcrobotEngine()
     x0 = eng.t(x0).reshape(-1, 4)
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, x0.shape[0], tol=tol, beta=beta, c=c, gamma_0=gamma_0,
-                                 max_ls=max_ls, hist_len=hist_len, pipeline=pipeline, persistent=persistent)
+                                 max_ls=max_ls, hist_len=hist_len, pipeline=pipeline, persistent=persistent,
+                                 capture_lanes=capture_lanes)
     return solver.solve(x0, max_iters, reduce_stats=reduce_stats)

@@ -12,7 +12,9 @@ argument order, defaults, return structure and error behaviour:
   calculate_K_and_sigma (:183)      -> gym_riccati_general
   forward_closed_loop_update (:218) -> gym_closed_loop
   total_cost (:231)                 -> gym_total_cost
-  plot_armijo_line_search (:254)    -> gym_gamma_sweep (the 200-rollout curve) + the reference's figure
+  plot_armijo_line_search (:254)    -> gym_gamma_sweep (the 200-rollout curve) + the line-search figure
+  generate_report_graphs (:405)     report figures from the results and history (matplotlib, optional);
+                                    plot_results (called by main.task_1, absent from the reference) = the same
   newton_Algorithm (:298)           -> gym_newton_init / gym_newton_iteration / gym_newton_finalize
   get_fully_actuated_ref (:511), compute_equilibrium (:22), define_reference_piecewise (:41)
                                     (problem setup on the host, as in the reference)
@@ -206,37 +208,118 @@ def plot_armijo_line_search(iteration, x_traj, u_traj, K, sigma, cost_current, x
     return curve
 
 
+_NON_INTERACTIVE = ("agg", "pdf", "ps", "svg", "cairo", "template")
+
+
+def _pyplot():
+    """matplotlib.pyplot, or None: the report figures are optional, the computed data is the result."""
+    try:
+        import matplotlib.pyplot as plt
+    except ImportError:
+        return None
+    return plt
+
+
+def _show(plt):
+    import matplotlib
+    if matplotlib.get_backend().lower() not in _NON_INTERACTIVE:
+        plt.show()
+
+
 def _draw_armijo(iteration, curve, cost_current, delta_J, gamma_accepted, stepsizes_tested, costs_tested, c, beta,
                  max_step):
-    try:
-        import matplotlib
-        import matplotlib.pyplot as plt
-    except ImportError:          # the report figure is optional; the curve is the computed result
+    """The line-search figure of :266-296: the cost along the direction, its first-order model, the Armijo line,
+    the tested step sizes and the accepted one."""
+    plt = _pyplot()
+    if plt is None:
         return
-    steps = curve["steps"]
-    plt.figure(f'Armijo Line Search - Iteration {iteration}', figsize=(12, 7))
-    plt.clf()
-    plt.plot(steps, curve["costs"], color='blue', linewidth=2.5,
-             label=r'$J(x_k + \gamma \cdot \delta x, u_k + \gamma \cdot \delta u)$', alpha=0.8)
-    plt.plot(steps, curve["linear_approx"], color='red', linewidth=2.5, linestyle='--',
-             label=r'$J_k + \gamma \cdot \nabla J^T \delta$', alpha=0.8)
-    plt.plot(steps, curve["armijo_line"], color='green', linestyle='--', linewidth=2.5,
-             label=rf'$J_k + c \cdot \gamma \cdot \nabla J^T \delta$ (c={c})', alpha=0.8)
+    fig, ax = plt.subplots(num=f"Armijo line search, iteration {iteration}", figsize=(12, 7), clear=True)
+    for key, style, label in (("costs", "-", r"$J(\gamma)$ along the Newton direction"),
+                              ("linear_approx", "--", r"$J_k + \gamma\,\Delta J$"),
+                              ("armijo_line", ":", rf"$J_k + c\,\gamma\,\Delta J$ (c = {c})")):
+        ax.plot(curve["steps"], curve[key], style, linewidth=2.2, label=label)
     if stepsizes_tested and costs_tested:
-        plt.scatter(stepsizes_tested, costs_tested, marker='*', s=150, color='orange', edgecolor='black',
-                    linewidth=1.5, zorder=5, label=rf'Tested stepsizes ($\beta$={beta})')
-        plt.scatter(gamma_accepted, costs_tested[-1], marker='o', s=200, color='red', edgecolor='black',
-                    linewidth=2.5, zorder=6, label=rf'Accepted: $\gamma$={gamma_accepted:.4f}')
-    plt.xlabel(r'Step Size $\gamma$', fontsize=14)
-    plt.ylabel('Cost Value J', fontsize=14)
-    plt.title(f'Armijo Line Search - Iteration {iteration}\n' +
-              f'Current Cost = {cost_current:.4f}, Expected Reduction = {delta_J:.2e}', fontsize=15)
-    plt.grid(True, alpha=0.3)
-    plt.legend(fontsize=12, loc='best')
-    plt.xlim(0, max_step)
-    plt.tight_layout()
-    if matplotlib.get_backend().lower() not in ("agg", "pdf", "ps", "svg", "cairo", "template"):
-        plt.show()
+        ax.scatter(stepsizes_tested, costs_tested, marker="*", s=140, zorder=5, label=rf"trials ($\beta$ = {beta})")
+        ax.scatter([gamma_accepted], [costs_tested[-1]], s=190, facecolors="none", edgecolors="k", linewidths=2,
+                   zorder=6, label=rf"accepted $\gamma$ = {gamma_accepted:.4f}")
+    ax.set(xlabel=r"step size $\gamma$", ylabel="cost J", xlim=(0, max_step),
+           title=f"iteration {iteration}: J = {cost_current:.4f}, expected reduction {delta_J:.2e}")
+    ax.grid(alpha=0.3)
+    ax.legend(loc="best")
+    fig.tight_layout()
+    _show(plt)
+
+
+def report_iterations(n_trajs: int) -> list:
+    """Iterations whose trajectories the report overlays (:440-448): 0, 1, 5, 10, 100 where they exist plus five
+    evenly spaced ones, ascending."""
+    fixed = [i for i in (0, 1, 5, 10, 100) if i < n_trajs]
+    even = np.linspace(0, n_trajs - 1, 5, dtype=int).tolist() if n_trajs else []
+    return sorted(set(fixed) | set(even))
+
+
+def generate_report_graphs(t_ref, x_ref, u_ref, x_opt, u_opt, history):
+    """The report figures of :405-509 from a solve's results and ``history`` (newton_Algorithm's, or a batched
+    lane's: SolveResult.x_trajs / hist_cost / hist_smax assembled into the same keys).
+
+    Four figures: optimal angles / torques against the desired curves; intermediate trajectories (the
+    iterations of ``report_iterations``); sigma_t of tau2 at the first and the last iterations; cost and
+    max|sigma| per iteration on log axes.  Drawn when matplotlib is importable (shown on interactive backends);
+    returns the plotted data either way."""
+    t_ref = np.asarray(t_ref, float)
+    x_ref, x_opt, u_opt = (np.asarray(a, float) for a in (x_ref, x_opt, u_opt))
+    u_ref = np.asarray(u_ref, float)
+    u_ref = u_ref[:-1] if u_ref.shape[0] == t_ref.shape[0] else u_ref
+    shown = report_iterations(len(history["x_trajs"]))
+    sig_its = sorted({i for i in (0, 1, 2, len(history["sigmas"]) - 1) if 0 <= i < len(history["sigmas"])})
+    data = {"iterations_shown": shown, "sigma_iterations": sig_its,
+            "sigma_tau2": {i: np.asarray(history["sigmas"][i], float).reshape(-1, 2)[:, 1] for i in sig_its},
+            "cost": np.asarray(history["cost"], float), "sigma_norm": np.asarray(history["sigma_norm"], float)}
+    plt = _pyplot()
+    if plt is None:
+        return data
+    tu = t_ref[:-1]
+    fig, (a0, a1) = plt.subplots(2, 1, num="optimal trajectory vs desired", figsize=(10, 8), clear=True)
+    for j, col in ((0, "tab:blue"), (1, "tab:red")):
+        a0.plot(t_ref, x_opt[:, j], color=col, linewidth=2, label=rf"$\theta_{j + 1}$ optimal")
+        a0.plot(t_ref, x_ref[:, j], color=col, linestyle="--", alpha=0.5, label=rf"$\theta_{j + 1}$ desired")
+        a1.step(tu, u_opt[:, j], color=("tab:green", "tab:purple")[j], label=rf"$\tau_{j + 1}$ optimal")
+        a1.step(tu, u_ref[:, j], color=("tab:green", "tab:purple")[j], linestyle="--", alpha=0.5,
+                label=rf"$\tau_{j + 1}$ desired")
+    a1.axhline(0.0, color="k", linewidth=1, alpha=0.5)
+    a0.set(ylabel="angle [rad]", title="optimal trajectory vs desired curve")
+    a1.set(ylabel="torque [Nm]", xlabel="time [s]")
+    fig2, axes = plt.subplots(2, 1, num="intermediate trajectories", figsize=(10, 7), clear=True)
+    for j, ax in enumerate(axes):
+        for i in shown:
+            ax.plot(t_ref, np.asarray(history["x_trajs"][i])[:, j], alpha=0.4, label=f"iter {i}")
+        ax.plot(t_ref, x_ref[:, j], "k--", linewidth=2, label="desired")
+        ax.set(ylabel=rf"$\theta_{j + 1}$ [rad]")
+    axes[0].set_title("intermediate trajectories vs desired")
+    axes[1].set_xlabel("time [s]")
+    fig3, a3 = plt.subplots(num="descent direction", figsize=(10, 5), clear=True)
+    for i, sg in data["sigma_tau2"].items():
+        a3.plot(tu, sg, label=rf"iter {i}: $\sigma_t$ ($\tau_2$)")
+    a3.set(xlabel="time [s]", ylabel="correction", title=r"descent direction $\sigma_t$ of $\tau_2$")
+    fig4, (b0, b1) = plt.subplots(1, 2, num="convergence", figsize=(12, 5), clear=True)
+    b0.semilogy(np.arange(len(data["cost"])), data["cost"], "o-", markersize=3)
+    b0.set(xlabel="iteration", ylabel="J", title="cost along iterations")
+    b1.semilogy(np.arange(1, len(data["sigma_norm"]) + 1), data["sigma_norm"], "o-", markersize=3, color="tab:red")
+    b1.set(xlabel="iteration", ylabel=r"$\|\sigma\|_\infty$", title="norm of the descent direction")
+    for f, axs in ((fig, (a0, a1)), (fig2, axes), (fig3, (a3,)), (fig4, (b0, b1))):
+        for ax in axs:
+            ax.grid(True, alpha=0.3)
+            if ax.get_legend_handles_labels()[0] and ax not in (b0, b1):
+                ax.legend(fontsize=9)
+        f.tight_layout()
+    data["figures"] = [fig, fig2, fig3, fig4]
+    _show(plt)
+    return data
+
+
+# main.task_1 calls tg.plot_results (main.py:49), which the reference module does not define (task 1 stops there
+# with AttributeError); here it draws the same report.
+plot_results = generate_report_graphs
 
 
 # ------------------------------------------------------------------------------ the solver
@@ -312,7 +395,26 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
 
 
 def newton_Algorithm_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gamma_0=1.0,
-                           max_ls=MAX_LINE_SEARCH_ITERS, hist_len=0, reduce_stats=None) -> SolveResult:
-    """Batched newton_Algorithm over lanes x0 (B,4) sharing (x_ref, u_ref) -> SolveResult (device tensors)."""
+                           max_ls=MAX_LINE_SEARCH_ITERS, hist_len=0, reduce_stats=None,
+                           capture_lanes=None) -> SolveResult:
+    """Batched newton_Algorithm over lanes x0 (B,4) sharing (x_ref, u_ref) -> SolveResult (device tensors).
+    ``hist_len`` keeps every lane's cost / max|sigma| history; ``capture_lanes`` keeps the listed lanes'
+    trajectories after every accepted iteration (SolveResult.x_trajs, the reference's history['x_trajs'])."""
     return newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=tol, beta=beta, c=c, gamma_0=gamma_0, max_ls=max_ls,
-                              engine=_eng(), hist_len=hist_len, reduce_stats=reduce_stats)
+                              engine=_eng(), hist_len=hist_len, reduce_stats=reduce_stats,
+                              capture_lanes=capture_lanes)
+
+
+def lane_history(res: SolveResult, lane: int) -> dict:
+    """The reference's ``history`` dict (:321-327) of one lane of a batched solve, for generate_report_graphs:
+    cost and sigma_norm from the per-lane histories (hist_len), x_trajs from capture_lanes.  'sigmas' holds the
+    lane's last-iteration sigma only (the batched solver does not keep every iteration's sigma)."""
+    if res.hist_cost is None or res.x_trajs is None or lane not in res.x_trajs:
+        raise ValueError("lane_history needs a solve with hist_len > 0 and the lane in capture_lanes")
+    n = int(res.n_iter[lane])
+    failed = int(res.status[lane]) == _lib.LS_FAILED
+    hc = res.hist_cost[:, lane].cpu().numpy()
+    hs = res.hist_smax[:, lane].cpu().numpy()
+    return {"cost": [res.cost0[lane]] + [float(v) for v in hc[:n - 1 if failed else n]],
+            "sigma_norm": [float(v) for v in hs[:n]], "x_trajs": res.x_trajs[lane],
+            "sigmas": [res.sigma[lane].cpu().numpy()]}

@@ -62,7 +62,7 @@ def compute_P_inf(A, B, Q, R):
     eng = _eng()
     P, it = eng.dare_fixed_point(A, B, Q, R, max_iter=1000, tol=1e-6)
     P = _np(P)
-    if int(it.item()) >= 1000 and not np.isfinite(P).all():
+    if int(it.item()) > 1000:                    # the tolerance was never met in 1000 iterations (:164)
         print("P_inf did not converge!!!")
     return P
 

@@ -27,10 +27,12 @@
  *                   states   x  : (N, Bp/64, 2, 64) double2   (th1, th2), (w1, w2)
  *                   gains    K1 : (T, Bp/64, 2, 64) double2   row 1 of K_t (row 0 is identically 0)
  *                   gains    Kf : (T, Bp/64, 4, 64) double2   full K_t: (K00,K01)(K02,K03)(K10,K11)(K12,K13)
- *                   offsets  cs : (T, Bp)           double2   (c1 = u1 - K1 x, sigma1) of the solver's sweep
  *     planes (W = 1): one component per element, (L, P, Bp)
  *                   controls u  : (T, 2, Bp) double    planes tau1, tau2
  *                   sigma    s  : (T, 2, Bp) double
+ *                   offsets  cs : (T, 2, Bp) double    planes cg = (u1 - K1 x) + gamma0 sigma1 (written by every
+ *                                                      solver sweep) and sigma1 (written only by the sigma1
+ *                                                      re-runs: backtracking lanes, gym_newton_sigma, gamma sweeps)
  */
 #ifndef GYMNAST_ACROBOT_H
 #define GYMNAST_ACROBOT_H
@@ -108,10 +110,10 @@ typedef struct gym_batch {
     int64_t B, Bp;      /* lanes, lane stride (multiple of 64)                     */
     int32_t N, hist_len;/* knots (T = N-1); rows of the optional history buffers   */
     int32_t flags, pad; /* GYM_FLAG_*                                               */
-    double* x[2];       /* (N,2,Bp) double2 state trajectories, double-buffered (wave-blocked) */
-    double* u[2];       /* (T,2,Bp) control planes, double-buffered               */
-    double* K1;         /* (T,2,Bp) double2 feedback gains, row 1 (wave-blocked)  */
-    double* cs;         /* (T,2,Bp) planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1 (re-run only) */
+    double* x[2];       /* (N, Bp/64, 2, 64) double2 state trajectories, wave-blocked pairs, double-buffered */
+    double* u[2];       /* (T, 2, Bp) control planes tau1, tau2, double-buffered  */
+    double* K1;         /* (T, Bp/64, 2, 64) double2 feedback gains, row 1, wave-blocked pairs */
+    double* cs;         /* (T, 2, Bp) planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1 (re-runs only) */
     const double* x_ref;/* (N,4) shared reference states                          */
     const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
     double* cost;       /* (Bp) current J_k                                       */
@@ -266,7 +268,8 @@ int gym_tv_lqr_gains(const double* A, const double* B, int32_t S, const double* 
                      const double Q[16], const double R[4], const double QT[16], int32_t L, int32_t nwin,
                      int32_t all_gains, int32_t discretize, double dt, double* K_out, void* stream);
 /* compute_P_inf (trajectory_tracking.py:144-165): P (4,4) and the iteration count [device outputs]; A, B discrete
- * [device], Q, R [host]. */
+ * [device], Q, R [host].  iters_out = the iteration at which max|P_next - P| < tol held, or max_iter + 1 if it never
+ * did (the reference then prints "P_inf did not converge!!!" and returns the last P, :164-165). */
 int gym_dare_fixed_point(const double* A, const double* B, const double Q[16], const double R[4], int32_t max_iter,
                          double tol, double* P_out, int32_t* iters_out, void* stream);
 /* solver_mpc's X_opt (L,4), U_opt (L-1,2): forward pass x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s of one window

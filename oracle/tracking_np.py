@@ -49,14 +49,15 @@ def riccati_step(A, B, P, Q, R):
 
 
 def compute_P_inf(A, B, Q, R, max_iter=1000, tol=1e-6):
-    """:144-165 (returns P and the iteration count; the reference prints if it did not converge)."""
+    """:144-165 (returns P and the iteration count, max_iter + 1 if the tolerance was never met: the reference
+    then prints 'P_inf did not converge!!!', :164)."""
     P = Q
     for i in range(max_iter):
         P_prev = P
         _, P = riccati_step(A, B, P, Q, R)
         if np.abs(P - P_prev).max() < tol:
             return P, i + 1
-    return P, max_iter
+    return P, max_iter + 1
 
 
 def solve_LQR_tracking(x_opt, u_opt, Q=Q_REG, R=R_REG, QT=QT_REG):

@@ -82,3 +82,97 @@ def test_sharded_loop_matches_single_process(tmp_path, world):
         np.testing.assert_array_equal(p["res"]["u"], r["u"][sl])
     assert r["status"][3] == 2 and r["n_iter"][3] == 1      # the NaN lane fails on its first iteration
     assert ref_log[-1][0] == 0 or ref.k == MAX_ITERS
+
+
+# ------------------------------------------------------------------ schedule choice and the persistent loop
+def test_schedule_lanes_identical_on_ragged_shards():
+    """Every rank bases the automatic schedule on the largest shard, so ragged shards (which differ by one lane)
+    can never straddle a threshold: 49,153 lanes on 2 ranks are 24,577 / 24,576, both ranks decide on 24,577."""
+    from gymnast_optimalcontrol_amd import distributed as gd
+    assert gd.schedule_lanes(49153, 2) == 24577
+    assert gd.schedule_lanes(49152, 2) == 24576
+    assert gd.schedule_lanes(7, 3) == 3
+    sizes = [gd.shard_range(49153, r, 2) for r in range(2)]
+    assert [hi - lo for lo, hi in sizes] == [24577, 24576]
+
+
+class _PersistentAdapter:
+    """The oracle stepper behind the persistent schedule's host loop (solver.run_loop): one ``_run(k0, k1)``
+    advances every lane by k1 - k0 iterations and leaves the 8 statistics on ``stats``."""
+
+    def __init__(self, stepper, chunk):
+        import torch
+        self.st, self.chunk, self.k, self._cap_pos = stepper, chunk, 0, None
+        self.stats = torch.zeros(24, dtype=torch.float64)
+
+    def _run(self, k0, k1):
+        import torch
+        from oracle.acrobot_np import ACTIVE
+        for _ in range(k0, k1):
+            if (self.st.status == ACTIVE).any():
+                self.stats[:8] = torch.from_numpy(self.st.iteration())
+            else:                                  # finished lanes: the kernel's iterations are no-ops
+                self.st.k += 1
+                self.stats[0] = 0.0
+
+    def _capture(self):
+        pass
+
+    def collect_timing(self):
+        pass
+
+
+def _persistent_worker(rank, world, port, out_path, chunk):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from gymnast_optimalcontrol_amd import distributed as gd
+    from gymnast_optimalcontrol_amd.solver import run_loop
+    from oracle.acrobot_np import NewtonStepper
+    gd.init_process_group(backend="gloo")
+    x0, x_ref, u_ref = _problem()
+    lo, hi = gd.shard_range(len(x0), rank, world)
+    ad = _PersistentAdapter(NewtonStepper(x0[lo:hi], x_ref, u_ref, tol=1e-4, gamma_0=0.1), chunk)
+    log = run_loop(ad, MAX_ITERS, gd.make_reduce_stats(), 0, True)
+    # an empty shard is refused on every rank before any collective (no rank left blocking in an all-reduce)
+    try:
+        gd.solve_sharded(np.zeros((world - 1, 4)), x_ref, u_ref, 5)
+        refused = False
+    except ValueError:
+        refused = True
+    gathered = [None] * world
+    dist.all_gather_object(gathered, dict(lo=lo, hi=hi, log=np.asarray(log), res=ad.st.result(), refused=refused))
+    if rank == 0:
+        np.save(out_path, np.array(gathered, dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunk", [(2, 4), (3, 7)])
+def test_persistent_loop_sharded_matches_single_process(tmp_path, world, chunk):
+    """The persistent schedule's host loop across ranks: one all-reduce per launch of ``chunk`` iterations on
+    every rank (ragged shards), the global stop after the launch in which the last lane of any rank finished,
+    and per-lane results equal to the single-process solve."""
+    from oracle.acrobot_np import NewtonStepper
+    out = str(tmp_path / "gathered.npy")
+    mp.start_processes(_persistent_worker, args=(world, _free_port(), out, chunk), nprocs=world, join=True,
+                       start_method="spawn")
+    parts = np.load(out, allow_pickle=True)          # written by this test's own workers
+    x0, x_ref, u_ref = _problem()
+    ref = NewtonStepper(x0, x_ref, u_ref, tol=1e-4, gamma_0=0.1)
+    from gymnast_optimalcontrol_amd.solver import newton_loop
+    newton_loop(ref, MAX_ITERS)
+    r = ref.result()
+    logs = [p["log"] for p in parts]
+    for lg in logs[1:]:
+        np.testing.assert_array_equal(lg, logs[0])   # the same all-reduced statistics at the same launches
+    assert len(logs[0]) == -(-int(r["n_iter"].max()) // chunk) or len(logs[0]) == -(-MAX_ITERS // chunk)
+    for p in parts:
+        assert p["refused"]
+        sl = slice(p["lo"], p["hi"])
+        np.testing.assert_array_equal(p["res"]["n_iter"], r["n_iter"][sl])
+        np.testing.assert_array_equal(p["res"]["status"], r["status"][sl])
+        np.testing.assert_array_equal(p["res"]["x"], r["x"][sl])

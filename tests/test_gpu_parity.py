@@ -5,6 +5,9 @@ i.e. the reference's arithmetic reordered, so per-primitive results agree to ~1e
 converged trajectories to ~1e-13; the north-star bar for converged trajectories is 1e-8 rel-L2.
 Discrete decisions (iteration counts, Armijo trials, statuses) must match exactly.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -247,43 +250,96 @@ def test_ragged_batches_and_padding(B, task2_refs):
     assert last[1] == pytest.approx(o["cost"].sum(), rel=1e-10)
 
 
+# Far from convergence (gamma_0 = 1, wide starts) Newton iterates amplify rounding-level differences from one
+# iteration to the next.  How much is a property of the problem, measured on runs of the reference itself
+# (tests/golden/wide_lanes.npz, make_golden_wide.py, 25 of these lanes): after 120 iterations (every such lane has
+# hit its Armijo failure by then) the C restatement's last iterate differs from the reference's by up to 5.5e-6
+# (x), 9.4e-6 (u), 1.3e-6 (K) and 2.7e-3 (sigma, the last Newton step, nearly cancelling) per lane -- lane 151
+# and 116 -- with every decision identical; after 12 iterations by <= 3e-13.  The bounds below are 10x those
+# reference-pinned spreads.  Decisions (iteration counts, statuses, rollout counts) must agree exactly on every
+# lane; a sigma taken from the wrong iterate would differ by O(1).
+WIDE_TOL = {12: dict(x=1e-11, u=1e-11, K=1e-11, sigma=1e-11, cost=1e-12),
+            120: dict(x=6e-5, u=1e-4, K=1.5e-5, sigma=3e-2, cost=2e-6)}
+
+
+def _decisions_agree(got, ref, what):
+    ni, st, nr = got
+    bad = np.flatnonzero((ni != ref["n_iter"]) | (st != ref["status"]) | (nr != ref["n_rollouts"]))
+    assert bad.size == 0, (f"{what}: decisions differ on lanes {bad.tolist()}: n_iter {ni[bad].tolist()} vs "
+                           f"{ref['n_iter'][bad].tolist()}, status {st[bad].tolist()} vs {ref['status'][bad].tolist()}, "
+                           f"rollouts {nr[bad].tolist()} vs {ref['n_rollouts'][bad].tolist()}")
+
+
+def _per_lane(got, ref):
+    n = got.shape[0]
+    return np.linalg.norm((got - ref).reshape(n, -1), axis=1) / \
+        np.maximum(np.linalg.norm(ref.reshape(n, -1), axis=1), 1e-300)
+
+
 @pytest.mark.parametrize("schedule", ["serial", "pipelined", "persistent"])
 @pytest.mark.parametrize("max_iters", [12, 120])
 def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, schedule, max_iters):
     """K and sigma of each lane's last iteration (newton_Algorithm's return values) after backtracking, LS
-    failures, a NaN lane and the max_iters cut-off.  sigma1 is not streamed by the solver: gym_newton_sigma
-    re-runs each lane's last sweep from the state buffer that iteration started from, and the lanes that
-    backtrack re-run theirs inside the iteration; both must reproduce the oracle's values."""
+    failures, a NaN lane and the max_iters cut-off, on 160 wide-start lanes with gamma_0 = 1.  sigma1 is not
+    streamed by the solver: gym_newton_sigma re-runs each lane's last sweep from the state buffer that iteration
+    started from, and the lanes that backtrack re-run theirs inside the iteration; both must reproduce the
+    oracle's values.  Every lane's decisions agree exactly; values within WIDE_TOL per lane."""
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
     from oracle import c_oracle
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden_wide import wide_x0
     xr, ur, _ = task2_refs
-    B = 160
-    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
-    x0[:20, 2:] = np.random.default_rng(6).uniform(-2.0, 2.0, (20, 2))      # seed-14-like lanes: early LS failures
-    x0[9] = np.nan
+    x0 = wide_x0()                                           # lanes 0-19 with initial velocities; lane 9 NaN
+    B = x0.shape[0]
     r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, gamma_0=1.0, pipeline=schedule == "pipelined",
                             persistent=schedule == "persistent").solve(x0, max_iters)
     o = c_oracle.newton_solve(x0, xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=1.0)
     ni, st = r.n_iter.cpu().numpy(), r.status.cpu().numpy()
-    same = (ni == o["n_iter"]) & (st == o["status"]) & (r.n_rollouts.cpu().numpy() == o["n_rollouts"])
-    assert same.mean() >= 0.97, f"decisions differ on {np.flatnonzero(~same)}"
+    _decisions_agree((ni, st, r.n_rollouts.cpu().numpy()), o, f"{schedule}, {max_iters} iterations")
     assert st[9] == _lib.LS_FAILED and np.isnan(r.sigma.cpu().numpy()[9]).any()
     assert (r.n_rollouts.cpu().numpy() > ni).any()                           # some lanes backtracked
     if max_iters == 120:
         assert (st == _lib.LS_FAILED).sum() >= 2
-    ok = same & np.isfinite(o["cost"])
-    # Far from convergence (gamma_0 = 1, wide starts) Newton iterates amplify rounding-level differences from
-    # iteration to iteration, so after 120 iterations the two implementations' iterates differ by ~1e-5
-    # relative; a sigma taken from the wrong iterate (the other state buffer) would differ by O(1).
-    tol = 1e-8 if max_iters <= 12 else 1e-3
+    ok = np.isfinite(o["cost"])
+    assert ok.sum() == B - 1
     for name, ref in (("sigma", o["sigma"]), ("K", o["K"]), ("x", o["x"]), ("u", o["u"])):
-        got = getattr(r, name).cpu().numpy()[ok]
-        assert rel_l2(got, ref[ok]) < tol, name
-        lane_err = np.linalg.norm((got - ref[ok]).reshape(ok.sum(), -1), axis=1) / \
-            np.maximum(np.linalg.norm(ref[ok].reshape(ok.sum(), -1), axis=1), 1e-300)
-        assert lane_err.max() < 10 * tol, (name, int(np.argmax(lane_err)))
+        err = _per_lane(getattr(r, name).cpu().numpy()[ok], ref[ok])
+        tol = WIDE_TOL[max_iters][name]
+        assert err.max() < tol, (name, int(np.flatnonzero(ok)[np.argmax(err)]), float(err.max()))
+
+
+@pytest.mark.parametrize("schedule", ["serial", "pipelined", "persistent"])
+@pytest.mark.parametrize("max_iters", [12, 120])
+def test_wide_start_lanes_vs_reference(golden, task2_refs, schedule, max_iters):
+    """16 of those lanes pinned to the REFERENCE itself (tests/golden/wide_lanes.npz: newton_Algorithm with
+    gamma_0 = 1, tol 1e-4, run in the build container): identical iteration counts, statuses and rollout counts
+    (backtracking and the Armijo failure of trajectory_generation.py:352-369), and last-iteration K, sigma, x, u
+    per lane within 10x the C restatement's own distance from the reference (no looser than WIDE_TOL)."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from oracle import c_oracle
+    W = golden("wide_lanes")
+    xr, ur, _ = task2_refs
+    m = f"m{max_iters}_"
+    x0 = W[m + "x0"]
+    ref = {"n_iter": W[m + "n_iter"], "status": W[m + "status"], "n_rollouts": W[m + "n_rollouts"]}
+    r = BatchedNewtonSolver(AcrobotEngine(), xr, ur, x0.shape[0], tol=1e-4, gamma_0=1.0,
+                            pipeline=schedule == "pipelined", persistent=schedule == "persistent").solve(x0, max_iters)
+    _decisions_agree((r.n_iter.cpu().numpy(), r.status.cpu().numpy(), r.n_rollouts.cpu().numpy()), ref,
+                     f"{schedule} vs reference, {max_iters} iterations")
+    o = c_oracle.newton_solve(x0, xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=1.0)
+    for name in ("K", "sigma", "x", "u"):
+        err = _per_lane(getattr(r, name).cpu().numpy(), W[m + name])
+        bound = np.minimum(np.maximum(10 * _per_lane(o[name], W[m + name]), 1e-11), WIDE_TOL[max_iters][name])
+        assert (err <= bound).all(), (name, np.flatnonzero(err > bound).tolist(), err.max())
+    n, st = W[m + "n_iter"], W[m + "status"]
+    # final cost = the last accepted entry of the reference's history['cost']
+    J = np.array([W[m + "cost_hist"][i, int(n[i]) - 1 if int(st[i]) == 2 else int(n[i])] for i in range(len(n))])
+    err = np.abs(r.cost.cpu().numpy() - J) / np.abs(J)
+    bound = np.minimum(np.maximum(10 * np.abs(o["cost"] - J) / np.abs(J), 1e-12), WIDE_TOL[max_iters]["cost"])
+    assert (err <= bound).all(), ("cost", np.flatnonzero(err > bound).tolist(), err.max())
 
 
 def test_single_trial_line_search_and_nan_lane(task2_refs):

@@ -42,6 +42,28 @@ def test_c_oracle_primitives_match_reference(golden):
         np.testing.assert_allclose(B, g["B_c"][i], rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("pset", [2, 3])
+def test_oracles_parameter_sets_match_reference(golden, pset):
+    """Parameter sets 2 / 3 (dynamics.py:31-61) through the reference's own set_params (:117-144), lambdified by
+    tests/golden/make_golden_wide.py: both oracles reproduce its dynamics, RK4 and Jacobians."""
+    from gymnast_optimalcontrol_amd.params import PARAM_NAMES, PARAM_SETS
+    g = golden("pset_kats")
+    X, U = g["X"], g["U"]
+    np.testing.assert_allclose(onp.continuous_dynamics(X, U, pset), g[f"p{pset}_f_cont"], rtol=1e-12, atol=1e-10)
+    np.testing.assert_allclose(onp.rk4(X, U, pset=pset), g[f"p{pset}_f_rk4"], rtol=1e-12, atol=1e-10)
+    A, B = onp.jacobians(X, U, pset)
+    np.testing.assert_allclose(A, g[f"p{pset}_A_c"], rtol=1e-11, atol=1e-9)
+    np.testing.assert_allclose(B, g[f"p{pset}_B_c"], rtol=1e-11, atol=1e-12)
+    params = tuple(PARAM_SETS[pset][k] for k in PARAM_NAMES)
+    for i in range(X.shape[0]):
+        np.testing.assert_allclose(oc.rk4(X[i], U[i], params), g[f"p{pset}_f_rk4"][i], rtol=1e-11, atol=1e-9)
+        A, B = oc.jacobians(X[i], U[i], params)
+        np.testing.assert_allclose(A, g[f"p{pset}_A_c"][i], rtol=1e-10, atol=1e-8)
+        np.testing.assert_allclose(B, g[f"p{pset}_B_c"][i], rtol=1e-10, atol=1e-12)
+    # the sets differ enough that a wrong set cannot pass
+    assert np.max(np.abs(g[f"p{pset}_f_rk4"] - golden("kat_primitives")["f_rk4"])) > 1e-3
+
+
 # ------------------------------------------------------------------------ one Newton iteration
 @pytest.mark.parametrize("tag", ["it0", "mid"])
 def test_numpy_oracle_newton_iteration(golden, tag):
@@ -143,3 +165,25 @@ def test_numpy_oracle_armijo_curve_matches_reference(golden):
     c1 = onp.gamma_sweep(g["k0_x"], g["k0_u"], g["k0_K"], g["k0_sigma"], g["k0_tested"], g["x_ref"],
                          g["u_ref"])
     np.testing.assert_allclose(c1, g["k0_costs_tested"], rtol=1e-13)
+
+
+@pytest.mark.parametrize("max_iters", [12, 120])
+def test_c_oracle_wide_start_lanes_match_reference(golden, task2_refs, max_iters):
+    """gamma_0 = 1 wide-start lanes run by the reference itself (make_golden_wide.py): the C restatement makes the
+    same decisions (iterations, LS failures, rollouts) on every lane; the values differ only by the rounding
+    amplification of the far-from-converged Newton iterates (the spreads the GPU tests' WIDE_TOL is built on)."""
+    W = golden("wide_lanes")
+    xr, ur, _ = task2_refs
+    m = f"m{max_iters}_"
+    o = oc.newton_solve(W[m + "x0"], xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=1.0)
+    np.testing.assert_array_equal(o["n_iter"], W[m + "n_iter"])
+    np.testing.assert_array_equal(o["status"], W[m + "status"])
+    np.testing.assert_array_equal(o["n_rollouts"], W[m + "n_rollouts"])
+    assert (W[m + "n_rollouts"] > W[m + "n_iter"]).all()             # every lane backtracked
+    if max_iters == 120:
+        assert (W[m + "status"] == 2).all()                            # ... and hit its Armijo failure
+    spread = {12: dict(x=1e-13, u=1e-13, K=1e-13, sigma=1e-12), 120: dict(x=6e-6, u=1e-5, K=1.5e-6, sigma=3e-3)}
+    for k in ("x", "u", "K", "sigma"):
+        a, b = o[k], W[m + k]
+        e = np.linalg.norm((a - b).reshape(len(a), -1), axis=1) / np.linalg.norm(b.reshape(len(b), -1), axis=1)
+        assert e.max() < spread[max_iters][k], (k, e.max())

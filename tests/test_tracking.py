@@ -135,3 +135,36 @@ def test_tracking_abi_rejects_bad_arguments():
     m = _lib.GymModel()
     assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 0, 501, 1, 1, None) == 1          # empty batch
     assert lib.gym_track_rollout(C.byref(m), 1, 1, 1, 1, 100, 1, 1, 1, None) == 1          # N < 2
+
+
+def _slow_pair():
+    """(A, B) whose fixed point does not settle in 1000 iterations: the last two states are uncontrollable and
+    marginally stable (A = I there), so P grows by Q each iteration -- finite, never within tol."""
+    A = np.eye(4)
+    A[0, 2] = A[1, 3] = 0.02
+    B = np.zeros((4, 2)); B[0, 0] = B[1, 1] = 0.05
+    return A, B
+
+
+def test_oracle_p_inf_reports_non_convergence():
+    from oracle import tracking_np as tr
+    A, B = _slow_pair()
+    P, it = tr.compute_P_inf(A, B, np.eye(4), np.eye(2))
+    assert it == 1001 and np.isfinite(P).all()
+    assert P[3, 3] > 1000.0                       # grows by at least Q_33 = 1 per iteration
+
+
+@pytest.mark.gpu
+def test_p_inf_prints_when_not_converged(capsys, trk):
+    """The reference prints 'P_inf did not converge!!!' whenever the 1000-iteration loop ends without meeting
+    the tolerance, and returns the (finite) last P (trajectory_tracking.py:164-165); on convergence it is
+    silent."""
+    from gymnast_optimalcontrol_amd import trajectory_tracking as tt
+    from oracle import tracking_np as tr
+    A, B = _slow_pair()
+    P = tt.compute_P_inf(A, B, np.eye(4), np.eye(2))
+    assert "P_inf did not converge!!!" in capsys.readouterr().out
+    Po, _ = tr.compute_P_inf(A, B, np.eye(4), np.eye(2))
+    np.testing.assert_allclose(P, Po, rtol=1e-12)
+    tt.compute_P_inf(trk["A_f"], trk["B_f"], trk["Q_mpc"], trk["R_mpc"])
+    assert "did not converge" not in capsys.readouterr().out

@@ -19,8 +19,11 @@ step() {  # step <name> <seconds> <cmd...>
 for s in "$@"; do
   case $s in
     smoke)  step smoke 400 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests)  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --tb=short ;;
-    bench)  step bench 600 python -u bench.py --steps 1 --warmup 1 --cpu-lanes 4096 ;;
+    tests)  step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --tb=short --timeout 300 --timeout-method thread ;;
+    newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_workloads.py tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --tb=short --timeout 300 --timeout-method thread -k "workloads or wide or vs_oracle or capture" ;;
+    bench)  step bench 600 python -u bench.py --steps 2 --warmup 1 --cpu-lanes 4096 ;;
+    bench_mpc) step bench_mpc 300 python -u bench.py --workload mpc --steps 20 --warmup 3 ;;
+    bench_cfg2) step bench_cfg2 300 python -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" ;;
     *) echo "unknown step $s" ;;
   esac
 done
