@@ -181,7 +181,8 @@ class NewtonLeg:
         self.solver = BatchedNewtonSolver(
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
-            schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero)
+            schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
+            split_waves=a.split_waves == "on")
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
@@ -320,6 +321,8 @@ def main():
                     help="solver schedule (auto: the solver's choice for the batch size)")
     ap.add_argument("--chunk", type=int, default=128,
                     help="persistent schedule: iterations per launch (0: all of max_iters in one)")
+    ap.add_argument("--split-waves", choices=("on", "off"), default="on",
+                    help="persistent schedule: two wavefronts per 64 lanes (k_nt_run2, default) or one (k_nt_run)")
     ap.add_argument("--u0-zero", choices=("auto", "off"), default="auto",
                     help="off: force the general kernels (tau1 planes streamed) for the main leg")
     a = ap.parse_args()

@@ -30,10 +30,11 @@ EXPORTS = (
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run")
 
-ABI_VERSION = 6         # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 7         # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
+FLAG_RUN_SINGLE = 4      # GYM_FLAG_RUN_SINGLE
 CKPT_INTERVAL = 4        # GYM_CKPT_INTERVAL
 
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4

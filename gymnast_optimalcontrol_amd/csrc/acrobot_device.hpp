@@ -54,17 +54,20 @@ __device__ __forceinline__ PolyRegs poly_vgprs() {
 }
 
 __device__ __forceinline__ double ksin(double r, double z, const PolyRegs& k) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     return fma(r * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.s6, k.s5),
         2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
         -1.66666666666666324348e-01), r);
 }
 __device__ __forceinline__ double kcos(double z, const PolyRegs& k) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     return fma(z * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.c6, k.c5),
         -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
         4.16666666666666019037e-02), fma(-0.5, z, 1.0));
 }
 
 __device__ __forceinline__ void fast_sincos(double x, double* s, double* c, const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     constexpr double kTwoOverPi = 6.36619772367581382433e-01;
     constexpr double kPio2Hi = 1.57079632679489655800e+00;   // 0x3FF921FB54442D18
     constexpr double kPio2Lo = 6.12323399573676603587e-17;   // 0x3C91A62633145C07
@@ -83,6 +86,7 @@ __device__ __forceinline__ void fast_sincos(double x, double* s, double* c, cons
 
 // 1/v for v in the well-conditioned range of det M: hardware reciprocal + two Newton steps.
 __device__ __forceinline__ double recip(double v) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     double r = __builtin_amdgcn_rcp(v);
     double e = fma(-v, r, 1.0);
     r = fma(r, e, r);
@@ -94,6 +98,7 @@ __device__ __forceinline__ double recip(double v) {
 // M/C/G/F of dynamics.py:63-90).  det M = d (a - d) - b^2 cos^2(th2) > 0 is formed without cancellation.
 __device__ __forceinline__ void accel(const Dyn& m, double th1, double th2, double w1, double w2, double tau2,
                                       double& q1, double& q2) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     double s1, c1, s2, c2;
     fast_sincos(th1, &s1, &c1);
     fast_sincos(th2, &s2, &c2);
@@ -111,6 +116,7 @@ __device__ __forceinline__ void accel(const Dyn& m, double th1, double th2, doub
 // accel() from precomputed sin/cos of both joint angles.
 __device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, double s2, double c2, double w1,
                                          double w2, double tau2, double& q1, double& q2) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     const double s12 = s1 * c2 + c1 * s2;            // sin(th1 + th2)
     const double bs2 = m.b * s2;
     const double M11 = m.a2b + 2.0 * m.b * c2;
@@ -128,6 +134,7 @@ __device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, dou
 // with |d| > pi/4 (|w| > 39 rad/s) reduces both arguments from scratch instead.  The choice is per lane,
 // so a lane's arithmetic never depends on which other lanes share its wavefront.
 __device__ __forceinline__ void rotate(double s, double c, double d, double& so, double& co, const PolyRegs& k) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     const double z = d * d;
     const double sd = ksin(d, z, k), cd = kcos(z, k);
     so = fma(s, cd, c * sd);
@@ -152,6 +159,7 @@ __device__ __forceinline__ void substep_sincos(double th1, double th2, double d1
 // h k3, get their sin/cos by angle addition (substep_sincos).
 __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2,
                                     const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     double a1, b1, a2, b2, a3, b3, a4, b4;
     double s1, c1, s2, c2, t1, u1, t2, u2;
     fast_sincos(x0, &s1, &c1, k);

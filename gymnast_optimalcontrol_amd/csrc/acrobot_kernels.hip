@@ -185,8 +185,18 @@ constexpr uint32_t WROW = BLK * 16;
 // stage cost exactly as total_cost accumulates it (:244-245): J += dx^T Q dx ; J += du^T R du
 __device__ __forceinline__ double xcost(const double* w, double n0, double n1, double n2, double n3,
                                         const double* xr) {
+#pragma clang fp contract(on)   // context-independent bits (the cost of k_nt_run2's helper wavefront)
     const double e0 = n0 - xr[0], e1 = n1 - xr[1], e2 = n2 - xr[2], e3 = n3 - xr[3];
     return ((e0 * (w[0] * e0) + e1 * (w[1] * e1)) + e2 * (w[2] * e2)) + e3 * (w[3] * e3);
+}
+// one stage of total_cost (:244-245) added to the running J, with FMA contraction inside each expression only:
+// the same bits in every kernel that accumulates a trial's cost
+__device__ __forceinline__ double stage_cost(double J, const double* Q, const double* R, double n0, double n1,
+                                            double n2, double n3, const double* xrt, double f0, double f1) {
+#pragma clang fp contract(on)
+    J += xcost(Q, n0, n1, n2, n3, xrt);
+    J += f0 * (R[0] * f0) + f1 * (R[1] * f1);
+    return J;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -226,8 +236,7 @@ __device__ __forceinline__ double rollout_ref(const Dyn& m, const KW& w, const d
         }
         const double* urt = ur + 2 * t;
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
-        J += xcost(w.Q, n0, n1, n2, n3, xr + 4 * t);
-        J += f0 * (w.R[0] * f0) + f1 * (w.R[1] * f1);
+        J = stage_cost(J, w.Q, w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
         gym::rk4(m, n0, n1, n2, n3, v1);
         if (WRITE) {
             xn[wix(t + 1, 0, 2, l, Bp)] = make_double2(n0, n1);
@@ -252,6 +261,30 @@ struct TrialStage {
     double cg, s1;       // offset cg, sigma1 (SIG only)
     double u0;           // tau1 control (0 when U0Z)
 };
+
+// The trial's controls of one stage, each with FMA contraction inside its expression only (the same bits in
+// every kernel, including k_nt_run2 where the helper wavefront forms u0 and the cost):
+//   u0_new = u0 + gamma sigma0,  sigma0 = -(2R0 (u0 - ur0)) / (2R0)  == the sweep's sigma0, bit for bit
+//   (U0Z: u0 = ur0 = 0  =>  u0_new = +0 exactly)
+__device__ __forceinline__ double trial_u0(double u0, double ur0, double gamma, double G00, double iG00) {
+#pragma clang fp contract(on)
+    const double s0 = -(G00 * (u0 - ur0)) * iG00;
+    return u0 + gamma * s0;
+}
+//   u1_new = cg + K1 x_new  (the first trial, gamma = gamma0)
+__device__ __forceinline__ double trial_u1(double2 k0, double2 k1, double cg, double n0, double n1, double n2,
+                                          double n3) {
+#pragma clang fp contract(on)
+    const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
+    return cg + kx;
+}
+//   u1_new = fma(gamma - gamma0, sigma1, cg + K1 x_new)  (any other step size)
+__device__ __forceinline__ double trial_u1_sig(double2 k0, double2 k1, double cg, double s1, double dg, double n0,
+                                              double n1, double n2, double n3) {
+#pragma clang fp contract(on)
+    const double kx = ((k0.x * n0 + k0.y * n1) + k1.x * n2) + k1.y * n3;
+    return __builtin_fma(dg, s1, cg + kx);
+}
 
 template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT, bool BAND = true>
 __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const double* __restrict__ u,
@@ -291,14 +324,12 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     auto body = [&](const TrialStage& q, int t) {
         prio_band<BAND ? 1 : PRIO_NONE>(t, T);
         const double* urt = ur + 2 * t;
-        const double s0 = -(G00 * (q.u0 - urt[0])) * iG00;   // == the sweep's sigma0, bit for bit
-        const double v0 = q.u0 + gamma * s0;                 // U0Z: u0 = ur0 = 0  =>  v0 = +0 exactly
-        const double kx = ((q.k0.x * n0 + q.k0.y * n1) + q.k1.x * n2) + q.k1.y * n3;
-        const double v1 = SIG ? __builtin_fma(dg, q.s1, q.cg + kx) : q.cg + kx;
+        const double v0 = trial_u0(q.u0, urt[0], gamma, G00, iG00);
+        const double v1 = SIG ? trial_u1_sig(q.k0, q.k1, q.cg, q.s1, dg, n0, n1, n2, n3)
+                              : trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
         const double f0 = v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
-        J += xcost(ka.w.Q, n0, n1, n2, n3, xr + 4 * t);
-        J += f0 * (ka.w.R[0] * f0) + f1 * (ka.w.R[1] * f1);
+        J = stage_cost(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
             if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
@@ -330,6 +361,27 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
 //   Q_t = 2Q, R_t = 2R (diagonal), S_t = 0  =>  G = diag(2R0, 2R1 + b^T P b), K_t row 0 = 0.
 // P is kept symmetric (10 registers), p and (optionally) the costate lambda in registers.
 // ------------------------------------------------------------------------------------------
+// Stage t's linearisation (build_stage_lists :166-181 with discretize_linearization :161-164): rows 2, 3 of
+// A_d = I + dt A_c (rows 0, 1 are [1 0 dt 0], [0 1 0 dt]), column 1 of B_d = dt B_c, q_t = 2Q dx_t, r_t = 2R du_t.
+// A function of x_t, u_t only (not of P), so it can be evaluated apart from the Riccati chain.
+struct Lin {
+    double A20, A21, A22, A23, A30, A31, A32, A33, bd2, bd3, q0, q1, q2, q3, r0, r1, dt;
+};
+__device__ __forceinline__ Lin stage_lin(const Dyn& m, const KW& w, const gym::Jac& J, double2 xa, double2 xb,
+                                         double ut0, double ut1, const double* xrt, const double* urt) {
+#pragma clang fp contract(on)
+    const double dt = m.h;
+    Lin L;
+    L.A20 = dt * J.a2[0]; L.A21 = dt * J.a2[1]; L.A22 = 1.0 + dt * J.a2[2]; L.A23 = dt * J.a2[3];
+    L.A30 = dt * J.a3[0]; L.A31 = dt * J.a3[1]; L.A32 = dt * J.a3[2]; L.A33 = 1.0 + dt * J.a3[3];
+    L.bd2 = dt * J.bc2; L.bd3 = dt * J.bc3;
+    L.q0 = w.twoQ[0] * (xa.x - xrt[0]); L.q1 = w.twoQ[1] * (xa.y - xrt[1]);
+    L.q2 = w.twoQ[2] * (xb.x - xrt[2]); L.q3 = w.twoQ[3] * (xb.y - xrt[3]);
+    L.r0 = w.G00 * (ut0 - urt[0]); L.r1 = w.twoR1 * (ut1 - urt[1]);
+    L.dt = dt;
+    return L;
+}
+
 template <bool LAMBDA>
 struct Sweep {
     double P00, P01, P02, P03, P11, P12, P13, P22, P23, P33, p0, p1, p2, p3;
@@ -357,18 +409,20 @@ struct Sweep {
     __device__ __forceinline__ void step_j(const Dyn& m, const KW& w, const gym::Jac& J, double2 xa, double2 xb,
                                            double ut0, double ut1, const double* xrt, const double* urt, double& k0,
                                            double& k1, double& k2, double& k3, double& s0, double& s1) {
+        step_lin(w, stage_lin(m, w, J, xa, xb, ut0, ut1, xrt, urt), k0, k1, k2, k3, s0, s1);
+    }
+    // the Riccati update of stage t from its linearisation (stage_lin: a function of x_t, u_t only)
+    __device__ __forceinline__ void step_lin(const KW& w, const Lin& L, double& k0, double& k1, double& k2,
+                                             double& k3, double& s0, double& s1) {
         // FMA contraction within each expression only, never across statements: the bits then do not depend on
         // the context the stage is compiled into (the interleaved sweep of backward_solver_lane_ilp, the sigma1
-        // re-runs) -- with cross-statement fusion they did
+        // re-runs, the two-wavefront sweep of k_nt_run2) -- with cross-statement fusion they did
 #pragma clang fp contract(on)
-        const double dt = m.h;
-        // A_d rows 2,3 (rows 0,1 = [1 0 dt 0], [0 1 0 dt]); B_d = dt * [0 0 bc2 bc3]^T in column 1
-        const double A20 = dt * J.a2[0], A21 = dt * J.a2[1], A22 = 1.0 + dt * J.a2[2], A23 = dt * J.a2[3];
-        const double A30 = dt * J.a3[0], A31 = dt * J.a3[1], A32 = dt * J.a3[2], A33 = 1.0 + dt * J.a3[3];
-        const double bd2 = dt * J.bc2, bd3 = dt * J.bc3;
-        const double q0 = w.twoQ[0] * (xa.x - xrt[0]), q1 = w.twoQ[1] * (xa.y - xrt[1]);
-        const double q2 = w.twoQ[2] * (xb.x - xrt[2]), q3 = w.twoQ[3] * (xb.y - xrt[3]);
-        const double r0 = w.G00 * (ut0 - urt[0]), r1 = w.twoR1 * (ut1 - urt[1]);
+        const double dt = L.dt;
+        const double A20 = L.A20, A21 = L.A21, A22 = L.A22, A23 = L.A23;
+        const double A30 = L.A30, A31 = L.A31, A32 = L.A32, A33 = L.A33;
+        const double bd2 = L.bd2, bd3 = L.bd3;
+        const double q0 = L.q0, q1 = L.q1, q2 = L.q2, q3 = L.q3, r0 = L.r0, r1 = L.r1;
         if (LAMBDA) {  // lambda_t = 2Q dx_t + A_d^T lambda_{t+1}
             const double n0 = q0 + (l0 + A20 * l2 + A30 * l3);
             const double n1 = q1 + (l1 + A21 * l2 + A31 * l3);
@@ -1471,6 +1525,14 @@ __device__ __forceinline__ void lane_fence() {   // this lane's stores visible t
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
 }
 
+#ifdef GYM_RUN2_TRACE
+// Diagnostic build only (tools/run2_trace.py): per workgroup and wavefront role, cycles (s_memtime) spent in the
+// sweep, the trial and the post-trial part, accumulated in registers and written once at the kernel's end.
+__device__ unsigned long long g_run2_trace[8192][2][6];
+#define R2T_NOW() __builtin_amdgcn_s_memtime()
+#else
+#define R2T_NOW() 0ull
+#endif
 template <bool U0Z>
 __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
     constexpr bool BAND = GYM_RUN_BAND == 1;
@@ -1479,7 +1541,10 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
     // Nothing but the lane index, the iteration counter and the lane's status stays live across a pass: J, dJ,
     // max|sigma| and x_0 are re-read from memory where needed (once per iteration).
     int st = run_args()->status[l];
+    unsigned long long acc[4] = {0, 0, 0, 0};   // GYM_RUN2_TRACE only: sweep / trial / post cycles, iterations
     for (int k = run_args()->k0; st == GYM_ACTIVE && k < run_args()->k1; ++k) {
+        unsigned long long tt = R2T_NOW();
+        ++acc[3];
         if (GYM_RUN_BAND == 2) {
             switch ((k >> 1) & 3) {
                 case 0: __builtin_amdgcn_s_setprio(3); break;
@@ -1504,6 +1569,8 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
             if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = s;
         }
         lane_fence();
+        acc[0] += R2T_NOW() - tt;
+        tt = R2T_NOW();
         double Jn;
         {
             const rargs_t R = run_args();
@@ -1512,6 +1579,7 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
                                                                    R->x[cb ^ 1], R->u[cb ^ 1], R->a.gamma0,
                                                                    R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y, xb.x, xb.y);
         }
+        acc[1] += R2T_NOW() - tt;
         const rargs_t R = run_args();
         double g = R->a.gamma0;
         int nr = 1;
@@ -1553,6 +1621,412 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
         }
         lane_fence();   // the candidate buffer is the next sweep's input
     }
+#ifdef GYM_RUN2_TRACE
+    if (threadIdx.x == 0 && blockIdx.x < 8192)
+        for (int i = 0; i < 4; ++i) g_run2_trace[blockIdx.x][0][i] = acc[i];
+#endif
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent schedule on TWO wavefronts per 64 lanes (k_nt_run2, the default persistent kernel).
+// In the latency-bound regime (BASELINE cfg 2: 4,096 lanes = 64 wavefronts on 1,024 SIMDs) every wavefront is
+// alone on its SIMD and issues about one fp64 instruction per 4.4-5 cycles (profiles/r02_probe/README.md), so a
+// stage costs its instruction count.  A second wavefront per 64 lanes, on another SIMD, takes every instruction
+// that is not on the lane's dependency chain:
+//   sweep : the helper evaluates stage t's Jacobian and linearisation (stage_lin: a function of x_t, u_t only)
+//           and hands them, with x_t and u_t, to the main wavefront through an LDS ring; the main wavefront runs
+//           only the Riccati recursion (step_lin) and stores K row 1 / cg;
+//   trial : the main wavefront runs the feedback + RK4 chain and hands (x_{t+1}, u1_t) to the helper, which
+//           forms u0, accumulates the cost and stores the candidate trajectory.
+// The two advance in chunks of R2C stages, the producer one chunk ahead (two chunks of ring slots), separated by
+// workgroup barriers; a chunk's ring slots hold R2W pairs per lane ([slot][pair][lane]: one 1 KiB row per wave
+// instruction).  Per lane the arithmetic is the single-wavefront kernel's -- the same functions (jacobian,
+// stage_lin, step_lin, trial_u0 / trial_u1, stage_cost, rk4), each contracting FMAs inside its expressions only
+// -- so the results are the same bits.  The rare Armijo retries (sigma1 re-run, trials 2..20) run on the main
+// wavefront alone, with the single-wavefront code, while the helper waits at the end-of-iteration barrier.
+// Lanes that are not active (finished, padding) run along without storing anything: every barrier is reached by
+// every thread, and the iteration loop ends when no lane of the workgroup is active.
+// ------------------------------------------------------------------------------------------
+#ifndef GYM_RUN2_C
+#define GYM_RUN2_C 2
+#endif
+constexpr int R2C = GYM_RUN2_C;   // stages per chunk (even)
+constexpr int R2S = 2 * R2C;      // ring slots
+constexpr int R2W = 11;           // pairs per lane and slot: sweep x_t (2), u_t, Lin (8); trial x_{t+1} (2), u1_t
+#ifndef GYM_RUN2_PD
+#define GYM_RUN2_PD 4
+#endif
+// Prefetch distance of the producers' stream loads, in stages (= register sets in rotation).  A stage of either
+// wavefront is now ~2x shorter than the single-wavefront kernel's, and the loads of data the previous pass wrote
+// take ~1 us: with one stage of prefetch both passes ran at the load latency (~2,400 cycles per stage measured,
+// whatever the instruction count, tools/run2_trace.py).
+constexpr int R2PD = GYM_RUN2_PD;
+#ifndef GYM_RUN2_DYN_SGPR
+#define GYM_RUN2_DYN_SGPR 0   // measurement variant: the trial's model coefficients held in SGPRs
+#endif
+static_assert(R2PD % R2C == 0, "the prefetch distance is a whole number of chunks");
+// chunks per pass, rounded up to whole register-set rotations: producer and consumer both run this many chunk
+// phases (the consumer skips the stages past T), so their barrier counts match
+// a stage index the compiler may compute on the VALU (e.g. a clamp as v_sub_u32 ... clamp) made wave-uniform
+// again: a buffer resource built from a VGPR value becomes a waterfall loop of v_readfirstlane
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// x_ref / u_ref rows through the constant address space: the compiler then reads a stage's row with scalar loads
+// (it cannot prove that no store of the kernel clobbers a plain global pointer, and falls back to vector loads
+// that count in vmcnt -- and the stage then waits for them behind its prefetches)
+typedef const __attribute__((address_space(4))) double* cptr_t;
+template <int NV>
+struct Row {
+    double v[NV];
+};
+template <int NV>
+__device__ __forceinline__ Row<NV> const_row(const double* base, int t) {
+    const cptr_t p = (cptr_t)base + (int64_t)NV * t;
+    Row<NV> r;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) r.v[i] = p[i];
+    return r;
+}
+__device__ __forceinline__ void in_vgpr2(double2& v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
+__device__ __forceinline__ int run2_chunks(int T) {
+    constexpr int per = R2PD / R2C;
+    return ((T + R2C - 1) / R2C + per - 1) / per * per;
+}
+typedef double2 (*ring_t)[R2W][BLK];
+
+// The chunk hand-off: this wavefront's LDS writes complete, then the workgroup barrier.  Not __syncthreads(): its
+// workgroup-scope release also drains every outstanding global load and store (s_waitcnt vmcnt(0)), i.e. the
+// next stages' prefetches and the last stores' round trip at every chunk.  Only LDS crosses between the two
+// wavefronts inside a pass; global memory is handed over at the iteration's end (lane_fence + __syncthreads).
+// The "memory" clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier(unsigned long long& wait) {
+    const unsigned long long t0 = R2T_NOW();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    wait += R2T_NOW() - t0;   // GYM_RUN2_TRACE only (otherwise 0 + 0: removed)
+}
+
+// helper wavefront HID of NH, sweep: the stages i = HID, HID + NH, ... of the reverse pass (t = T-1-i) into slot
+// (chunk & 1) * R2C + (i % R2C)
+template <bool U0Z, int HID, int NH>
+__device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t l, int cb, const double* __restrict__ xr,
+                                                  const double* __restrict__ ur, unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)R->Bp * 16u, plane = (uint32_t)R->Bp * 8u;
+    const char* Xb = reinterpret_cast<const char*>(R->x[cb]);
+    const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
+    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them)
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    auto fetch = [&](SweepStage& q, int t) {
+        const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)t * row);
+        q.xa = bld2(rX, o2, 0);
+        q.xb = bld2(rX, o2, WROW);
+        q.u0 = U0Z ? 0.0 : bld1(rU, o1, 0);
+        q.u1 = bld1(rU, o1, plane);
+    };
+    auto produce = [&](const SweepStage& q, int t, int slot) {
+        const KArgs ka = kernarg_consts();
+        const gym::Jac J = gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
+        const Row<4> xrt = const_row<4>(xr, t);
+        const Row<2> urt = const_row<2>(ur, t);
+        const Lin L = stage_lin(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
+        double2(*s)[BLK] = ring[slot];
+        s[0][lane] = q.xa;                          s[1][lane] = q.xb;
+        s[2][lane] = make_double2(q.u0, q.u1);      s[3][lane] = make_double2(L.A20, L.A21);
+        s[4][lane] = make_double2(L.A22, L.A23);    s[5][lane] = make_double2(L.A30, L.A31);
+        s[6][lane] = make_double2(L.A32, L.A33);    s[7][lane] = make_double2(L.bd2, L.bd3);
+        s[8][lane] = make_double2(L.q0, L.q1);      s[9][lane] = make_double2(L.q2, L.q3);
+        s[10][lane] = make_double2(L.r0, L.r1);
+    };
+    // Branch-free stream loads: every producer stage loads (a clamped stage index past the end), so the
+    // compiler's wait-count tracking stays exact and a stage waits only for its own loads, R2PD stages old
+    // (with loads on conditional paths it fell back to vmcnt(0) at every stage: the prefetch was void).
+    static_assert(R2C % NH == 0, "every helper takes the same number of stages per chunk");
+    const int nch = run2_chunks(T);
+    SweepStage P[R2PD / NH];               // stage i's streams in set (i % R2PD) / NH, loaded R2PD stages ahead
+#pragma unroll
+    for (int j = HID; j < R2PD; j += NH) fetch(P[j / NH], uni(max(T - 1 - j, 0)));
+    for (int c0 = 0; c0 < nch; c0 += R2PD / R2C) {
+#pragma unroll
+        for (int cc = 0; cc < R2PD / R2C; ++cc) {
+            const int c = c0 + cc;
+#pragma unroll
+            for (int j = HID; j < R2C; j += NH) {
+                const int i = c * R2C + j, set = (cc * R2C + j) / NH;
+                // the stage's streams moved out of the loading registers first (the only wait: for this set, R2PD
+                // stages old), so that the set is re-armed at once and every later use reads the copy
+                SweepStage w = P[set];
+                in_vgpr2(w.xa); in_vgpr2(w.xb); gym::in_vgpr(w.u0); gym::in_vgpr(w.u1);
+                fetch(P[set], uni(max(T - 1 - (i + R2PD), 0)));
+                produce(w, uni(max(T - 1 - i, 0)), (c & 1) * R2C + j);   // past the end: not consumed
+            }
+            lds_barrier(bw);
+        }
+    }
+    lds_barrier(bw);
+}
+
+// main wavefront, sweep: the Riccati recursion from the ring; K row 1 / cg stored for active lanes
+template <bool U0Z>
+__device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l, int cb, bool act, double& dJ_out,
+                                                double& smax_out, unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double g0 = R->a.gamma0;
+    const double2* x = R->x[cb];
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], R->xr + 4 * T);
+    const int nch = run2_chunks(T);
+    lds_barrier(bw);                       // the helper's chunk 0
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            const int i = c * R2C + j;
+            if (i < T) {
+                const double2(*s)[BLK] = ring[(c & 1) * R2C + j];
+                const double2 xa = s[0][lane], xb = s[1][lane], uu = s[2][lane];
+                const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
+                const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
+                const KArgs ka = kernarg_consts();
+                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
+                            qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
+                double k0, k1, k2, k3, s0, s1;
+                S.step_lin(ka.w, L, k0, k1, k2, k3, s0, s1);
+                if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, k0, k1, k2,
+                                                 k3, s1);
+            }
+        }
+        lds_barrier(bw);
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// main wavefront, first Armijo trial: feedback + RK4 chain; (x_{t+1}, u1_t) into the ring
+template <bool U0Z>
+__device__ __forceinline__ void run2_trial_main(ring_t ring, int lane, int64_t l, int cb, unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    auto fetch = [&](TrialStage& q, int t) {
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        q.k0 = bld2(rK, o2, 0);
+        q.k1 = bld2(rK, o2, WROW);
+        q.cg = bld1(rsrc(Cb + (int64_t)t * row), o1, 0);
+    };
+    const gym::PolyRegs pk = gym::poly_vgprs();
+#if GYM_RUN2_DYN_SGPR
+    const Dyn dm = R->m;                   // held in SGPRs across the stage loop
+#endif
+    auto step = [&](const TrialStage& q, int slot) {
+        const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
+#if GYM_RUN2_DYN_SGPR
+        gym::rk4(dm, n0, n1, n2, n3, v1, pk);
+#else
+        const KArgs ka = kernarg_consts();
+        gym::rk4(ka.m, n0, n1, n2, n3, v1, pk);
+#endif
+        double2(*s)[BLK] = ring[slot];
+        s[0][lane] = make_double2(n0, n1);
+        s[1][lane] = make_double2(n2, n3);
+        s[2][lane] = make_double2(v1, 0.0);
+    };
+    const int nch = run2_chunks(T);        // branch-free stream loads (see run2_sweep_helper)
+    TrialStage P[R2PD];                    // stage t's streams in set t % R2PD, loaded R2PD stages ahead
+#pragma unroll
+    for (int j = 0; j < R2PD; ++j) fetch(P[j], uni(min(j, T - 1)));
+    for (int c0 = 0; c0 < nch; c0 += R2PD / R2C) {
+#pragma unroll
+        for (int cc = 0; cc < R2PD / R2C; ++cc) {
+            const int c = c0 + cc;
+#pragma unroll
+            for (int j = 0; j < R2C; ++j) {
+                const int t = c * R2C + j, set = cc * R2C + j;
+                step(P[set], (c & 1) * R2C + j);   // past the end: harmless, not consumed
+                fetch(P[set], uni(min(t + R2PD, T - 1)));
+            }
+            lds_barrier(bw);
+        }
+    }
+    lds_barrier(bw);
+}
+
+// helper wavefront, first Armijo trial: u0, the running cost and the candidate's stores; returns J
+template <bool U0Z>
+__device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64_t l, int cb, bool act,
+                                                  const double* __restrict__ xr, const double* __restrict__ ur,
+                                                  unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
+    const char* Xb = reinterpret_cast<const char*>(R->x[cb ^ 1]);
+    const char* Ob = reinterpret_cast<const char*>(R->u[cb ^ 1]);
+    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them)
+    const double gamma = R->a.gamma0;
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    if (act) {
+        const auto rX = rsrc(Xb);
+        bst2(rX, o2, 0, n0, n1);
+        bst2(rX, o2, WROW, n2, n3);
+    }
+    double J = 0.0;
+    const int nch = run2_chunks(T);
+    lds_barrier(bw);                       // the main wavefront's chunk 0
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            const int t = c * R2C + j;
+            if (t < T) {
+                const double2(*s)[BLK] = ring[(c & 1) * R2C + j];
+                const double2 na = s[0][lane], nb = s[1][lane], vv = s[2][lane];
+                const Row<2> urt = const_row<2>(ur, t);
+                const Row<4> xrt = const_row<4>(xr, t);
+                const KArgs ka = kernarg_consts();
+                const double u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
+                const double v0 = trial_u0(u0, urt.v[0], gamma, ka.w.G00, ka.w.iG00);
+                const double v1 = vv.x;
+                const double f0 = v0 - urt.v[0], f1 = v1 - urt.v[1];
+                J = stage_cost(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
+                if (act) {
+                    const auto rO = rsrc(Ob + (int64_t)t * row);
+                    if (!U0Z) bst1(rO, o1, 0, v0);
+                    bst1(rO, o1, plane, v1);
+                    const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
+                    bst2(rX, o2, 0, na.x, na.y);
+                    bst2(rX, o2, WROW, nb.x, nb.y);
+                }
+                n0 = na.x; n1 = na.y; n2 = nb.x; n3 = nb.y;
+            }
+        }
+        lds_barrier(bw);
+    }
+    const Row<4> xrT = const_row<4>(xr, T);
+    return J + xcost(R->w.QT, n0, n1, n2, n3, xrT.v);
+}
+
+#ifndef GYM_RUN2_HELPERS
+#define GYM_RUN2_HELPERS 2
+#endif
+constexpr int R2H = GYM_RUN2_HELPERS;   // helper wavefronts: the sweep's stages are dealt to them round-robin
+static_assert(R2H == 1 || R2H == 2, "one or two helper wavefronts");
+
+// a helper wavefront that has no part in a pass still takes part in its chunk barriers
+__device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
+    const int nch = run2_chunks(T);
+    for (int c = 0; c <= nch; ++c) lds_barrier(bw);
+}
+
+template <bool U0Z>
+__global__ __launch_bounds__((1 + R2H) * BLK, 1) void k_nt_run2(RunArgs args) {
+    __shared__ double2 ring[R2S][R2W][BLK];
+    __shared__ double shJ[BLK];
+    __shared__ int shst[BLK];
+    const int lane = threadIdx.x & (BLK - 1);
+    const int wave = threadIdx.x / BLK;          // 0: main; 1 .. R2H: helpers
+    const bool helper = wave > 0;
+    const int64_t l = (int64_t)blockIdx.x * BLK + lane;   // < Bp: padding lanes hold GYM_PAD
+    int st = run_args()->status[l];
+    // GYM_RUN2_TRACE only: sweep / trial / post cycles, iterations, barrier waits in the sweep / the trial
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = run_args()->k0; k < run_args()->k1; ++k) {
+        if (!__syncthreads_or(st == GYM_ACTIVE)) break;    // workgroup-uniform
+        const bool act = st == GYM_ACTIVE;
+        const int cb = k & 1;
+        unsigned long long tt = R2T_NOW();
+        ++acc[3];
+        if (wave == 1) {
+            run2_sweep_helper<U0Z, 0, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
+        } else if (wave == 2) {
+            run2_sweep_helper<U0Z, R2H - 1, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
+        } else {
+            double d, s;
+            run2_sweep_main<U0Z>(ring, lane, l, cb, act, d, s, acc[4]);
+            const rargs_t Q = run_args();
+            if (act) {
+                Q->dJ[l] = d;
+                Q->smax[l] = s;
+                if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = s;
+            }
+            lane_fence();                                  // K1 / cg visible to this wavefront's trial loads
+        }
+        acc[0] += R2T_NOW() - tt;
+        tt = R2T_NOW();
+        if (wave == 1) {
+            shJ[lane] = run2_trial_helper<U0Z>(ring, lane, l, cb, act, run_args()->xr, run_args()->ur, acc[5]);
+        } else if (wave == 2) {
+            run2_idle(run_args()->N - 1, acc[5]);
+        } else {
+            run2_trial_main<U0Z>(ring, lane, l, cb, acc[5]);
+        }
+        __syncthreads();                                   // shJ written; the helper's stores are complete
+        acc[1] += R2T_NOW() - tt;
+        tt = R2T_NOW();
+        if (!helper && act) {
+            const rargs_t R = run_args();
+            double Jn = shJ[lane];
+            double g = R->a.gamma0;
+            int nr = 1;
+            bool ok = Jn < R->cost[l] + R->a.c * g * R->dJ[l];   // strict Armijo test (:361)
+            if (!ok && R->a.max_ls > 1) {
+                lane_fence();                              // the helper's candidate stores, before they are rewritten
+                {
+                    const rargs_t P = run_args();
+                    double d2, s2;
+                    backward_solver_lane<U0Z, OUT_SIGMA, false>(P->m, P->w, P->x[cb], P->u[cb], P->xr, P->ur, P->K1,
+                                                                P->cs, 0.0, l, P->Bp, P->N, d2, s2);
+                }
+                lane_fence();
+                for (int j = 1; !ok && j < run_args()->a.max_ls; ++j) {
+                    const rargs_t P = run_args();
+                    g *= P->a.beta;                        // gamma_i *= beta, sequentially (:365)
+                    const double2 xa = P->x[cb][wix(0, 0, 2, l, P->Bp)], xb = P->x[cb][wix(0, 1, 2, l, P->Bp)];
+                    Jn = rollout_cform<true, U0Z, true, false, kNT, false>(P->m, P->w, P->u[cb], P->K1, P->cs, P->xr,
+                                                                          P->ur, P->x[cb ^ 1], P->u[cb ^ 1], g,
+                                                                          P->a.gamma0, l, P->Bp, P->N, xa.x, xa.y,
+                                                                          xb.x, xb.y);
+                    ++nr;
+                    const rargs_t Q = run_args();
+                    ok = Jn < Q->cost[l] + Q->a.c * g * Q->dJ[l];
+                }
+            }
+            const rargs_t F = run_args();
+            F->n_roll[l] += nr;
+            F->n_iter[l] += 1;
+            SolverCtl c = F->a;
+            c.k = k;
+            if (ok) {
+                const double sm = F->smax[l];
+                accept_lane(c, l, Jn, g, sm, F->cost, F->gamma, F->status, F->res_buf, F->hist_cost, F->Bp);
+                if (sm < c.tol) st = GYM_CONVERGED;
+            } else {
+                fail_lane(c, l, F->status, F->res_buf);
+                st = GYM_LS_FAILED;
+            }
+        }
+        if (!helper) shst[lane] = st;
+        lane_fence();                                      // every store of this iteration visible to both wavefronts
+        __syncthreads();
+        if (helper) st = shst[lane];
+        acc[2] += R2T_NOW() - tt;
+    }
+#ifdef GYM_RUN2_TRACE
+    if (lane == 0 && blockIdx.x < 8192 && wave <= 1)
+        for (int i = 0; i < 6; ++i) g_run2_trace[blockIdx.x][wave][i] = acc[i];
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2071,7 +2545,10 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
         ra.status = b->status; ra.n_iter = b->n_iter; ra.res_buf = b->res_buf; ra.n_roll = b->n_roll;
         ra.hist_cost = hist ? b->hist_cost : nullptr; ra.hist_smax = hist ? b->hist_smax : nullptr;
         ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.pad = 0;
-        hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
+        if (b->flags & GYM_FLAG_RUN_SINGLE)
+            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
+        else   // two wavefronts per 64 lanes; every lane of the padded batch takes part (padding: GYM_PAD)
+            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3((1 + R2H) * BLK), 0, st, ra);
     }
     // the statistics after iteration k1 - 1 ("lanes that ran" = the lanes that executed it; [4] = 0: this
     // schedule keeps no retry list)
@@ -2163,6 +2640,15 @@ int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_a
     return launch_status();
 }
 
+#ifdef GYM_RUN2_TRACE
+int gym_debug_run2_trace(void* host_out, int reset) {   // diagnostic build only: 8192 x 2 x 6 uint64
+    if (reset) {
+        static unsigned long long zero[8192][2][6];
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_run2_trace), zero, sizeof(zero));
+    }
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_run2_trace), sizeof(g_run2_trace));
+}
+#endif
 #ifdef GYM_WAVE_TRACE
 int gym_debug_wave_trace(void* host_out) {   // diagnostic build only: 2 x 8192 x 4 uint64
     return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wave_trace), sizeof(g_wave_trace));

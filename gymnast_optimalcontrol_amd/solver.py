@@ -91,7 +91,7 @@ class BatchedNewtonSolver:
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
-                 capture_lanes=None, capture_every: int = 1):
+                 capture_lanes=None, capture_every: int = 1, split_waves: bool = True):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -153,7 +153,11 @@ class BatchedNewtonSolver:
         # solve() works on the lanes in the Morton order of their initial states (see morton_order)
         self.reorder = bool(reorder)
         self.lane_order = None
-        b.flags =(_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0)
+        # persistent schedule on two wavefronts per 64 lanes (k_nt_run2: a helper wavefront takes the Jacobians,
+        # the cost and the stores off the lanes' dependency chains; same bits) unless split_waves=False
+        self.split_waves = bool(split_waves)
+        b.flags = ((_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0) |
+                   (0 if self.split_waves else _lib.FLAG_RUN_SINGLE))
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
         for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
@@ -270,17 +274,18 @@ class BatchedNewtonSolver:
         self._capture(initial=True)
 
     def _capture(self, initial: bool = False):
-        """Enqueue a gather of the captured lanes' current iterates (state buffer res_buf[lane]), their
-        iteration counts and statuses.  Device work only: no host synchronisation."""
+        """Enqueue a gather of the captured lanes' current iterates, their iteration counts, statuses and costs.
+        Device work only: no host synchronisation."""
         if self._cap_pos is None or (not initial and self.k % self.capture_every):
             return
         pos = self._cap_pos
         W = self.Bp // 64
         # wave-blocked pairs: (N, Bp/64, 2 rows, 64 lanes, 2) -> (n_cap, N, 2, 2) per buffer (the advanced
         # indices' dimension leads)
-        xs = [xb.view(self.N, W, 2, 64, 2)[:, pos // 64, :, pos % 64, :] for xb in self.x]
-        sel = self.res_buf[pos].to(torch.bool) if not initial else torch.zeros_like(pos, dtype=torch.bool)
-        x = torch.where(sel.view(-1, 1, 1, 1), xs[1], xs[0]).reshape(-1, self.N, 4)
+        # after k iterations a lane that accepted iteration k-1 holds its iterate in buffer k & 1 (iteration k-1
+        # wrote its candidate there); the records of lanes that did not are discarded by captured_trajectories
+        xb = self.x[self.k & 1]
+        x = xb.view(self.N, W, 2, 64, 2)[:, pos // 64, :, pos % 64, :].reshape(-1, self.N, 4)
         self._cap_log.append((self.k, x.clone(), self.n_iter[pos].clone(), self.status[pos].clone(),
                               self.cost[pos].clone()))
 

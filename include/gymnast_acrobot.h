@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 6
+#define GYM_ABI_VERSION 7
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -59,6 +59,8 @@ extern "C" {
                              * MI355X the solver kernels are VALU- as much as HBM-bound and it measured 13%
                              * slower).  The other knots of x[] are stale until gym_newton_fill_states
                              * rebuilds them (gym_newton_finalize does so itself).                          */
+#define GYM_FLAG_RUN_SINGLE 4 /* gym_newton_run: the single-wavefront persistent kernel instead of the default
+                               * two-wavefront one (helper wavefront per 64 lanes; same bits) */
 #define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 

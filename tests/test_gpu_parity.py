@@ -420,11 +420,13 @@ def test_pipelined_schedule_matches_serial(task2_refs, max_iters):
 
 
 @pytest.mark.parametrize("max_iters,chunk,u0z", [(25, 0, True), (5000, 0, True), (5000, 7, False), (5000, 0, False)])
-def test_persistent_schedule_matches_serial(task2_refs, max_iters, chunk, u0z):
+@pytest.mark.parametrize("split", [True, False])
+def test_persistent_schedule_matches_serial(task2_refs, max_iters, chunk, u0z, split):
     """The persistent schedule (gym_newton_run: each lane's iterations back to back in one launch per chunk, its
     Armijo trials 2..max_ls sequential) gives bitwise the serial schedule's lanes -- trajectories, last-iteration
     K and sigma, costs, decisions, rollout counts, per-lane histories -- incl. backtracking / LS-failure / NaN
-    lanes, the max_iters cut-off and chunked launches."""
+    lanes, the max_iters cut-off and chunked launches -- on the two-wavefront kernel (k_nt_run2, default) and the
+    single-wavefront one (GYM_FLAG_RUN_SINGLE)."""
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
@@ -435,7 +437,8 @@ def test_persistent_schedule_matches_serial(task2_refs, max_iters, chunk, u0z):
     eng = AcrobotEngine()
     kw = dict(tol=1e-4, gamma_0=0.1, u0_zero=None if u0z else False, hist_len=64)
     rs = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, **kw).solve(x0, max_iters, keep_stats=True)
-    rr = BatchedNewtonSolver(eng, xr, ur, B, persistent=True, chunk=chunk, **kw).solve(x0, max_iters, keep_stats=True)
+    rr = BatchedNewtonSolver(eng, xr, ur, B, persistent=True, chunk=chunk, split_waves=split,
+                             **kw).solve(x0, max_iters, keep_stats=True)
     for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax"):
         a, b = getattr(rs, name).cpu().numpy(), getattr(rr, name).cpu().numpy()
         assert np.array_equal(a, b, equal_nan=True), name

@@ -132,8 +132,8 @@ def test_capture_lanes_reproduce_reference_history(schedule, task2_refs):
     assert r.schedule == schedule
     tr = r.x_trajs
     assert len(tr[0]) == len(g["cost_hist"]) == 394
-    for j, it in enumerate(g["x_hist_idx"]):
-        assert rel_l2(tr[0][it], g["x_hist"][j]) < TOL_TRAJ, it
+    for j, it in enumerate(g["x_hist_idx"]):     # x_0 of the golden lane is the rest state: all zeros
+        np.testing.assert_allclose(tr[0][it], g["x_hist"][j], rtol=TOL_TRAJ, atol=1e-12, err_msg=str(it))
     np.testing.assert_array_equal(tr[0][-1], r.x[0].cpu().numpy())
     assert int(r.status[33]) == _lib.LS_FAILED
     assert len(tr[33]) == int(r.n_iter[33])                # x_0 + (n_iter - 1) accepted iterations
