@@ -25,16 +25,17 @@ EXPORTS = (
     "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase", "gym_newton_run",
     "gym_newton_finalize", "gym_newton_fill_states", "gym_newton_sigma",
     "gym_gamma_sweep", "gym_newton_gamma_sweep",
-    "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_lq_forward", "gym_track_rollout",
+    "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_mpc_gains", "gym_lq_forward", "gym_track_rollout", "gym_track_rollout_ex",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run")
 
-ABI_VERSION = 7         # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 8         # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
 FLAG_RUN_SINGLE = 4      # GYM_FLAG_RUN_SINGLE
+TRACK_SINGLE = 1         # GYM_TRACK_SINGLE
 CKPT_INTERVAL = 4        # GYM_CKPT_INTERVAL
 
 ACTIVE, CONVERGED, LS_FAILED, MAX_ITERS, PAD = 0, 1, 2, 3, 4
@@ -101,8 +102,10 @@ _SIGS = {
     "gym_newton_gamma_sweep": [_MP, _WP, _AP, _BP, _I32, _P, _I32, _P, _P],
     "gym_tv_lqr_gains": [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _D, _P, _P],
     "gym_dare_fixed_point": [_P, _P, _P, _P, _I32, _D, _P, _P, _P],
+    "gym_mpc_gains": [_MP, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _I32, _D, _P, _P, _P, _P],
     "gym_lq_forward": [_P, _P, _I32, _P, _P, _I32, _D, _P, _P, _I32, _P, _P, _P],
     "gym_track_rollout": [_MP, _P, _P, _P, _P, _I64, _I32, _P, _P, _P],
+    "gym_track_rollout_ex": [_MP, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P, _P],
     "gym_timing_create": [C.POINTER(GymTiming)],
     "gym_timing_destroy": [C.POINTER(GymTiming)],
     "gym_timing_collect": [C.POINTER(GymTiming)],

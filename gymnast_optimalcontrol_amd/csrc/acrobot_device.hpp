@@ -53,15 +53,33 @@ __device__ __forceinline__ PolyRegs poly_vgprs() {
     return k;
 }
 
+// Horner step fma(z, p, c) with a constant addend c.  GYM_HORNER_VOP3 (set by a translation unit before this
+// header) emits it as a three-address v_fma_f64 with c held in a VGPR: the compiler otherwise forms the
+// two-address v_fmac_f64 (accumulator = addend) and, c being live across the loop, copies it first with a
+// v_mov_b64 at every step (8 per rotation).  Same operation, same bits.  Every operand is a plain VGPR and the
+// result is consumed by ordinary VALU code (never directly by DPP), so no hazard is hidden in the asm.
+#ifndef GYM_HORNER_VOP3
+#define GYM_HORNER_VOP3 0
+#endif
+__device__ __forceinline__ double hfma(double z, double p, double c) {
+#if GYM_HORNER_VOP3
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "v"(c));
+    return r;
+#else
+    return fma(z, p, c);
+#endif
+}
+
 __device__ __forceinline__ double ksin(double r, double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(r * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.s6, k.s5),
+    return fma(r * z, hfma(z, hfma(z, hfma(z, hfma(z, fma(z, k.s6, k.s5),
         2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
         -1.66666666666666324348e-01), r);
 }
 __device__ __forceinline__ double kcos(double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(z * z, fma(z, fma(z, fma(z, fma(z, fma(z, k.c6, k.c5),
+    return fma(z * z, hfma(z, hfma(z, hfma(z, hfma(z, fma(z, k.c6, k.c5),
         -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
         4.16666666666666019037e-02), fma(-0.5, z, 1.0));
 }
@@ -173,6 +191,68 @@ __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double
     accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
     const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
     substep_sincos(x0, x1, m.h * z2, m.h * z3, s1, c1, s2, c2, t1, u1, t2, u2, k);
+    accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
+    const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
+    const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;
+    const double n2 = x2 + (m.h * (((a1 + 2.0 * a2) + 2.0 * a3) + a4)) * m.h6;
+    const double n3 = x3 + (m.h * (((b1 + 2.0 * b2) + 2.0 * b3) + b4)) * m.h6;
+    x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+}
+
+// ------------------------------------------------------------------------------------------
+// One trajectory on a lane pair (lanes 2p, 2p+1 of a wavefront): RK4 with the joint-angle trigonometry split.
+// For a latency-bound rollout (one wavefront per SIMD, each step a dependent chain) the wave's instruction
+// count per step is its time.  Both lanes hold the whole state; the even lane reduces / rotates the joint-1
+// angle, the odd lane the joint-2 angle, and four DPP broadcasts inside the quad give both lanes all four
+// sin/cos values; the accelerations and the update are evaluated by both (the same inputs, the same code:
+// the same bits).  Every value is the one gym::rk4 computes with the same operations, so the result is
+// bit-identical to rk4() (tested); ~200 instead of ~290 fp64 instructions per lane and step.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>   // DPP move of a double (two 32-bit halves) within quads
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double pair_even(double v) { return dpp_d<0xA0>(v); }   // quad_perm [0,0,2,2]
+__device__ __forceinline__ double pair_odd(double v) { return dpp_d<0xF5>(v); }    // quad_perm [1,1,3,3]
+
+// substep_sincos() on a lane pair: this lane's angle tho (th1 on the even lane, th2 on the odd one), its
+// base sin/cos (so, co) and the angle increments d1, d2 of both joints (both lanes: the same branch)
+__device__ __forceinline__ void substep_sincos_pair(bool odd, double tho, double d1, double d2, double so, double co,
+                                                    double& t1, double& u1, double& t2, double& u2,
+                                                    const PolyRegs& k) {
+    constexpr double kPio4 = 0.78539816339744830962;
+    const double d = odd ? d2 : d1;
+    double to, uo;
+    if (__builtin_expect(fabs(d1) <= kPio4 && fabs(d2) <= kPio4, 1)) {
+        rotate(so, co, d, to, uo, k);
+    } else {   // also taken by NaN lanes
+        fast_sincos(tho + d, &to, &uo, k);
+    }
+    t1 = pair_even(to); u1 = pair_even(uo);
+    t2 = pair_odd(to);  u2 = pair_odd(uo);
+}
+
+__device__ __forceinline__ void rk4_pair(const Dyn& m, bool odd, double& x0, double& x1, double& x2, double& x3,
+                                         double tau2, const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
+    double a1, b1, a2, b2, a3, b3, a4, b4;
+    double t1, u1, t2, u2;
+    const double tho = odd ? x1 : x0;
+    double so, co;
+    fast_sincos(tho, &so, &co, k);
+    const double s1 = pair_even(so), c1 = pair_even(co), s2 = pair_odd(so), c2 = pair_odd(co);
+    accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
+    const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
+    substep_sincos_pair(odd, tho, m.h2 * x2, m.h2 * x3, so, co, t1, u1, t2, u2, k);
+    accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
+    const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
+    substep_sincos_pair(odd, tho, m.h2 * y2, m.h2 * y3, so, co, t1, u1, t2, u2, k);
+    accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
+    const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
+    substep_sincos_pair(odd, tho, m.h * z2, m.h * z3, so, co, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
     const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
     const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;

@@ -14,6 +14,9 @@
 
 #include <cstdint>
 
+#ifndef GYM_HORNER_VOP3
+#define GYM_HORNER_VOP3 1   // three-address Horner steps (acrobot_device.hpp): no per-step constant copies
+#endif
 #include "acrobot_device.hpp"
 #include "gymnast_acrobot.h"
 
@@ -163,6 +166,142 @@ __global__ __launch_bounds__(64) void k_dare_fixed_point(const double* __restric
     if (ln == 0) *iters = it;
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused MPC gains (solve_mpc_tracking :14-38 + the exact solution of every control step's QP): one launch.
+//
+// Every stage matrix the MPC uses is the acrobot's discretised linearisation (:18-23, the pad (A_f, B_f) :31-33),
+// so it has a fixed structure: A_d rows 0,1 = [1,0,h,0], [0,1,0,h] (I + dt A_c with A_c rows e3', e4'),
+// B_d = [0, b] with b = (0, 0, b2, b3)' (tau1 unactuated, dynamics.py:205).  The Riccati map
+//   aux1 = R + B'PB, aux2 = B'PA, K = -inv(aux1) aux2, P <- Q + A'PA + (A'PB) K            (:158-160)
+// then needs, per entry, only the terms those zeros leave (the skipped products are exact zeros / ones in the
+// dense form; rounding of the rest is the reference's up to sum order, checked against the oracle at 1e-9).
+//
+// Lane-parallel map: a 16-lane group evaluates one map; lane 4i+j owns P[i][j] and the (i, j) entry of every
+// product.  Row i of P comes from the lane's own quad (DPP quad broadcasts); rows 2, 3 and i&1 of PA and PB
+// come from the group's other quads through ds_swizzle (no LDS storage, no barrier).  A map is then ~35 fp64
+// instructions per lane and a handful of exchanges on the critical path, instead of ~400 dependent flops of one
+// lane (k_tv_lqr_gains) or three LDS round trips with barriers (k_dare_fixed_point).
+// ------------------------------------------------------------------------------------------
+struct StageLin {
+    double a2[4], a3[4], b2, b3;   // rows 2, 3 of A_d; B_d[2][1], B_d[3][1]
+};
+
+// Calculate_A_B_matrixes + discretize_linearization (dynamics.py:217-226, trajectory_generation.py:161-164):
+// A_d = I + dt A_c, B_d = dt B_c, with the same operations as load_stage() on k_point's Jacobians
+__device__ __forceinline__ void disc_stage(const Dyn& m, double x0, double x1, double x2, double x3, double tau2,
+                                           StageLin& s) {
+    const gym::Jac J = gym::jacobian(m, x0, x1, x2, x3, tau2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        s.a2[j] = (j == 2 ? 1.0 : 0.0) + m.h * J.a2[j];
+        s.a3[j] = (j == 3 ? 1.0 : 0.0) + m.h * J.a3[j];
+    }
+    s.b2 = m.h * J.bc2;
+    s.b3 = m.h * J.bc3;
+}
+
+using gym::dpp_d;
+template <int AND, int OR>   // ds_swizzle bit mode inside 32-lane halves: lane' = (lane & AND) | OR
+__device__ __forceinline__ double swz_d(double v) {
+    constexpr int pat = (AND & 31) | ((OR & 31) << 5);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)b, pat);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), pat);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// per-lane constants of the map: lane 4i+j of its group
+struct MapLane {
+    double c0j, c1j;   // A_d[0][j], A_d[1][j]
+    double ci;         // A_d[0][i] + A_d[1][i] (exactly one of the two is nonzero): 1, 1, h, h
+    double Qij, R00, R01, R10, R11;
+};
+__device__ __forceinline__ MapLane map_lane(int i, int j, double h, const M44& Q, const M22& R) {
+    MapLane c;
+    c.c0j = j == 0 ? 1.0 : (j == 2 ? h : 0.0);
+    c.c1j = j == 1 ? 1.0 : (j == 3 ? h : 0.0);
+    c.ci = i < 2 ? 1.0 : h;
+    c.Qij = Q.v[4 * i + j];
+    c.R00 = R.v[0]; c.R01 = R.v[1]; c.R10 = R.v[2]; c.R11 = R.v[3];
+    return c;
+}
+
+// One Riccati map on the structured stage (a2j = A_d[2][j], a3j = A_d[3][j], a2i = A_d[2][i], a3i = A_d[3][i]);
+// returns P_next[i][j] and this lane's column j of the gain K (K0j, K1j).
+__device__ __forceinline__ double riccati_map_lane(double P, const MapLane& c, double a2j, double a3j, double a2i,
+                                                   double a3i, double b2, double b3, double& K0j, double& K1j) {
+#pragma clang fp contract(on)
+    // the gain's critical path is P -> PB -> aux1 -> 1/det -> K: PB and its exchanges are issued first
+    const double P2 = dpp_d<0xAA>(P), P3 = dpp_d<0xFF>(P);                    // P[i][2], P[i][3]
+    const double PB = P2 * b2 + P3 * b3;                                      // (PB)[i][1]; (PB)[i][0] = 0
+    const double PB2 = swz_d<0x10, 0x08>(PB), PB3 = swz_d<0x10, 0x0C>(PB);
+    const double P0 = dpp_d<0x00>(P), P1 = dpp_d<0x55>(P);
+    const double PA = ((P0 * c.c0j + P1 * c.c1j) + P2 * a2j) + P3 * a3j;     // (PA)[i][j]
+    const double a1 = c.R11 + (b2 * PB2 + b3 * PB3);                           // aux1[1][1]; aux1[0][*] = R[0][*]
+    const double idet = gym::recip(c.R00 * a1 - c.R01 * c.R10);              // rcp + 2 Newton steps
+    const double PA2 = swz_d<0x13, 0x08>(PA), PA3 = swz_d<0x13, 0x0C>(PA), PAh = swz_d<0x17, 0x00>(PA);
+    const double PBh = swz_d<0x14, 0x00>(PB);
+    const double a2 = b2 * PA2 + b3 * PA3;                                    // aux2[1][j]; aux2[0][j] = 0
+    K0j = -((-c.R01 * idet) * a2);                                            // -(inv(aux1) aux2)[0][j]
+    K1j = -((c.R00 * idet) * a2);                                             // -(inv(aux1) aux2)[1][j]
+    const double APA = (c.ci * PAh + a2i * PA2) + a3i * PA3;                  // (A'PA)[i][j]
+    const double APB = (c.ci * PBh + a2i * PB2) + a3i * PB3;                  // (A'PB)[i][1]; [i][0] = 0
+    return (c.Qij + APA) + APB * K1j;
+}
+
+constexpr int kMpcMaxStages = 256;   // LDS stage table of one workgroup: its 4 windows' stages (L + 2 <= 256)
+
+// Workgroup = 4 windows (16 lanes each).  1) every stage the 4 windows use, discretised, into LDS (one lane per
+// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by every group (the same
+// bits in every workgroup: no grid-wide dependency);  3) each window's recursion from P = P_inf over stages
+// w+L-2 .. w;  its first gain is the QP's solution u0 = K x0 at control step w.
+__global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restrict__ x_ref,
+                                                  const double* __restrict__ u_ref, int S,
+                                                  const double* __restrict__ xf, const double* __restrict__ uf,
+                                                  M44 Q, M22 R, int L, int nwin, int max_iter, double tol,
+                                                  double* __restrict__ K_out, double* __restrict__ QT_out,
+                                                  int32_t* __restrict__ iters_out) {
+    __shared__ StageLin st[kMpcMaxStages];
+    __shared__ StageLin pad;
+    const int ln = threadIdx.x, g = ln >> 4, i = (ln >> 2) & 3, j = ln & 3;
+    const int w0 = blockIdx.x * 4;
+    const int nst = min(3 + L - 1, kMpcMaxStages);      // local stages 0 .. 3 + L - 2
+    if (ln == 0) disc_stage(m, xf[0], xf[1], xf[2], xf[3], uf[1], pad);
+    for (int s = ln; s < nst; s += 64) {
+        const int gs = w0 + s;
+        if (gs < S) {
+            disc_stage(m, x_ref[4 * (int64_t)gs], x_ref[4 * (int64_t)gs + 1], x_ref[4 * (int64_t)gs + 2],
+                       x_ref[4 * (int64_t)gs + 3], u_ref[2 * (int64_t)gs + 1], st[s]);
+        }
+    }
+    __syncthreads();
+    const MapLane c = map_lane(i, j, m.h, Q, R);
+    // compute_P_inf on the pad stage, from P = Q
+    const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2, fb3 = pad.b3;
+    double P = c.Qij, K0j, K1j;
+    int it = max_iter + 1;                                // the tolerance was never met
+    for (int n = 0; n < max_iter; ++n) {
+        const double nP = riccati_map_lane(P, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
+        const bool conv = __all(fabs(nP - P) < tol);     // np.abs(P - P_prev).max() < tol (a NaN entry fails)
+        P = nP;
+        if (conv) { it = n + 1; break; }
+    }
+    if (blockIdx.x == 0 && ln < 16) {
+        QT_out[ln] = P;
+        if (ln == 0) *iters_out = it;
+    }
+    // window w0 + g: stages w + L - 2 .. w (local g + L - 2 .. g), pad past S
+    const int w = w0 + g;
+    for (int s = L - 2; s >= 0; --s) {
+        const StageLin* q = (w + s < S) ? &st[g + s] : &pad;
+        P = riccati_map_lane(P, c, q->a2[j], q->a3[j], q->a2[i], q->a3[i], q->b2, q->b3, K0j, K1j);
+    }
+    if (w < nwin && i == 0) {
+        K_out[8 * (int64_t)w + j] = K0j;
+        K_out[8 * (int64_t)w + 4 + j] = K1j;
+    }
+}
+
 // LQ forward pass of one window (solver_mpc's X_opt, U_opt): x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s
 __global__ void k_lq_forward(const double* __restrict__ A, const double* __restrict__ Bm, int S,
                              const double* __restrict__ Ap, const double* __restrict__ Bp, int disc, double dt,
@@ -231,6 +370,49 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
     }
 }
 
+// k_track_rollout with each trajectory on a lane pair (gym::rk4_pair): 2B threads, 128 B... of one lane's rows
+// split between the pair (even lane: (th1, th2) and u; odd lane: (w1, w2)).  The chain of 500 dependent RK4 steps
+// is the whole cost of this latency-bound kernel (B/32 wavefronts, one per SIMD), and the split shortens each
+// step's instruction stream by ~1/3.  Bit-identical to k_track_rollout (tested).
+__global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* __restrict__ x0,
+                                                           const double* __restrict__ x_ff,
+                                                           const double* __restrict__ u_ff,
+                                                           const double* __restrict__ K, int64_t B, int N,
+                                                           double* __restrict__ xo, double* __restrict__ uo) {
+    const int64_t th = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t l = th >> 1;
+    const bool odd = th & 1;
+    if (l >= B) return;                    // both lanes of a pair, so the pair's DPP partners are always active
+    const int T = N - 1;
+    double2* xl = reinterpret_cast<double2*>(xo + 4 * (int64_t)N * l) + (odd ? 1 : 0);
+    double2* ul = reinterpret_cast<double2*>(uo + 2 * (int64_t)T * l);
+    double n0 = x0[4 * l], n1 = x0[4 * l + 1], n2 = x0[4 * l + 2], n3 = x0[4 * l + 3];
+    xl[0] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+    double k[8], r[4], f[2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) k[q] = K[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
+    f[0] = u_ff[0]; f[1] = u_ff[1];
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    for (int t = 0; t < T; ++t) {
+        const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
+        const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
+        const double v1 = f[1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+        if (t + 1 < T) {
+            const double* kn = K + 8 * (t + 1);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) k[q] = kn[q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = x_ff[4 * (t + 1) + q];
+            f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
+        }
+        if (!odd) ul[t] = make_double2(v0, v1);
+        gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
+        xl[2 * (t + 1)] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+    }
+}
+
 inline M44 m44(const double* p) { M44 m; for (int i = 0; i < 16; ++i) m.v[i] = p[i]; return m; }
 inline M22 m22(const double* p) { M22 m; for (int i = 0; i < 4; ++i) m.v[i] = p[i]; return m; }
 inline int launch_status() { return (int)hipGetLastError(); }
@@ -258,6 +440,17 @@ int gym_dare_fixed_point(const double* A, const double* Bm, const double Q[16], 
     return launch_status();
 }
 
+int gym_mpc_gains(const gym_model* m, const double* x_ref, const double* u_ref, int32_t S, const double* x_f,
+                  const double* u_f, const double Q[16], const double R[4], int32_t L, int32_t nwin, int32_t max_iter,
+                  double tol, double* K_out, double* QT_out, int32_t* iters_out, void* s) {
+    if (!m || !x_ref || !u_ref || !x_f || !u_f || !Q || !R || !K_out || !QT_out || !iters_out || S <= 0 || L < 2 ||
+        L + 2 > kMpcMaxStages || nwin <= 0 || max_iter <= 0)
+        return GYM_EINVAL;
+    hipLaunchKernelGGL(k_mpc_gains, dim3((unsigned)((nwin + 3) / 4)), dim3(64), 0, (hipStream_t)s, Dyn(*m), x_ref,
+                       u_ref, S, x_f, u_f, m44(Q), m22(R), L, nwin, max_iter, tol, K_out, QT_out, iters_out);
+    return launch_status();
+}
+
 int gym_lq_forward(const double* A, const double* Bm, int32_t S, const double* A_pad, const double* B_pad,
                    int32_t discretize, double dt, const double* K, const double* x0, int32_t L, double* X, double* U,
                    void* s) {
@@ -268,13 +461,23 @@ int gym_lq_forward(const double* A, const double* Bm, int32_t S, const double* A
     return launch_status();
 }
 
+int gym_track_rollout_ex(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff,
+                         const double* K, int64_t B, int32_t N, int32_t flags, double* x_out, double* u_out, void* s) {
+    if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || B > ((int64_t)1 << 30) || N < 2 ||
+        (flags & ~GYM_TRACK_SINGLE))
+        return GYM_EINVAL;
+    if (flags & GYM_TRACK_SINGLE)
+        hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, Dyn(*m), x0,
+                           x_ff, u_ff, K, B, N, x_out, u_out);
+    else
+        hipLaunchKernelGGL(k_track_rollout_pair, dim3((unsigned)((2 * B + 63) / 64)), dim3(64), 0, (hipStream_t)s,
+                           Dyn(*m), x0, x_ff, u_ff, K, B, N, x_out, u_out);
+    return launch_status();
+}
+
 int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
                       int64_t B, int32_t N, double* x_out, double* u_out, void* s) {
-    if (!m || !x0 || !x_ff || !u_ff || !K || !x_out || !u_out || B <= 0 || B > ((int64_t)1 << 31) || N < 2)
-        return GYM_EINVAL;
-    hipLaunchKernelGGL(k_track_rollout, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)s, Dyn(*m), x0, x_ff,
-                       u_ff, K, B, N, x_out, u_out);
-    return launch_status();
+    return gym_track_rollout_ex(m, x0, x_ff, u_ff, K, B, N, 0, x_out, u_out, s);
 }
 
 }  // extern "C"

@@ -348,6 +348,25 @@ class AcrobotEngine:
                    "gym_dare_fixed_point")
         return P, it
 
+    def mpc_gains(self, x_ref, u_ref, x_f, u_f, Q, R, L: int, nwin: int, max_iter: int = 1000, tol: float = 1e-6):
+        """Fused MPC gains (gym_mpc_gains): stage linearisations of (x_ref, u_ref) and of the pad (x_f, u_f),
+        Q_T = compute_P_inf(A_f, B_f, Q, R), and each window's first gain.  Returns device tensors
+        (K0 (nwin,2,4), Q_T (4,4), iterations (1,) int32); no host synchronisation."""
+        x_ref = self.t(x_ref).reshape(-1, 4); u_ref = self.t(u_ref).reshape(-1, 2)
+        x_f = self.t(x_f).reshape(4); u_f = self.t(u_f).reshape(2)
+        S = x_ref.shape[0] - 1
+        if u_ref.shape[0] < S:
+            raise ValueError(f"u_ref must hold {S} stages, got {u_ref.shape[0]}")
+        Qh, Rh = self._host_mat(Q, 4, "Q"), self._host_mat(R, 2, "R")
+        K = torch.empty((nwin, 2, 4), dtype=F64, device=self.device)
+        P = torch.empty((4, 4), dtype=F64, device=self.device)
+        it = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.gym_mpc_gains(C.byref(self.model), x_ref.data_ptr(), u_ref.data_ptr(), S, x_f.data_ptr(),
+                                          u_f.data_ptr(), Qh.ctypes.data, Rh.ctypes.data, int(L), int(nwin),
+                                          int(max_iter), float(tol), K.data_ptr(), P.data_ptr(), it.data_ptr(),
+                                          self.stream), "gym_mpc_gains")
+        return K, P, it
+
     def lq_forward(self, A, Bm, K, x0, L: int, A_pad=None, B_pad=None, discretize: bool = False):
         """One window's LQ forward pass: X (L,4), U (L-1,2)."""
         A = self.t(A).reshape(-1, 4, 4); Bm = self.t(Bm).reshape(-1, 4, 2)
@@ -361,8 +380,9 @@ class AcrobotEngine:
                                            X.data_ptr(), U.data_ptr(), self.stream), "gym_lq_forward")
         return X, U
 
-    def track_rollout(self, x0, x_ff, u_ff, K):
-        """Batched closed-loop tracking: x0 (B,4) -> x (B,N,4), u (B,T,2) under the shared (x_ff, u_ff, K)."""
+    def track_rollout(self, x0, x_ff, u_ff, K, single: bool = False):
+        """Batched closed-loop tracking: x0 (B,4) -> x (B,N,4), u (B,T,2) under the shared (x_ff, u_ff, K).
+        single: one lane per trajectory instead of a lane pair (bit-identical; measurement / tests)."""
         x0 = self.t(x0).reshape(-1, 4)
         x_ff = self.t(x_ff).reshape(-1, 4); u_ff = self.t(u_ff).reshape(-1, 2); K = self.t(K).reshape(-1, 2, 4)
         N = x_ff.shape[0]
@@ -371,7 +391,8 @@ class AcrobotEngine:
         B = x0.shape[0]
         x = torch.empty((B, N, 4), dtype=F64, device=self.device)
         u = torch.empty((B, N - 1, 2), dtype=F64, device=self.device)
-        _lib.check(self.lib.gym_track_rollout(C.byref(self.model), x0.data_ptr(), x_ff.data_ptr(), u_ff.data_ptr(),
-                                              K.data_ptr(), B, N, x.data_ptr(), u.data_ptr(), self.stream),
-                   "gym_track_rollout")
+        _lib.check(self.lib.gym_track_rollout_ex(C.byref(self.model), x0.data_ptr(), x_ff.data_ptr(),
+                                                 u_ff.data_ptr(), K.data_ptr(), B, N,
+                                                 _lib.TRACK_SINGLE if single else 0, x.data_ptr(), u.data_ptr(),
+                                                 self.stream), "gym_track_rollout_ex")
         return x, u

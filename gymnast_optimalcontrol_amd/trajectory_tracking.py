@@ -30,6 +30,7 @@ R_MPC = np.diag([1e-6, 10.0])                       # :37
 X_F = np.array([np.pi, 0.0, 0.0, 0.0])              # :31
 U_F = np.array([0.0, 0.0])                          # :32
 T_PRED = 75                                         # :10
+MPC_FUSED_MAX_STAGES = 256                          # gym_mpc_gains: T_pred + 2 stages per workgroup's LDS table
 
 
 def _eng():
@@ -114,8 +115,13 @@ def mpc_gains(x_ref, u_ref, T_pred: int = T_PRED, Q=Q_MPC, R=R_MPC, n_steps: int
     u_ref = eng.t(u_ref).reshape(-1, 2)
     S = x_ref.shape[0] - 1                                          # A_list: one stage per u_ref row (:19)
     n_steps = S if n_steps is None else int(n_steps)
+    x_f, u_f = _final_state(eng)
+    if int(T_pred) + 2 <= MPC_FUSED_MAX_STAGES:
+        # one launch: stage linearisations, compute_P_inf and every window's recursion (gym_mpc_gains)
+        K0, QT, _ = eng.mpc_gains(x_ref, u_ref, x_f, u_f, Q, R, L=int(T_pred), nwin=n_steps)
+        return K0, QT
     A_c, B_c = eng.jacobians(x_ref[:S], u_ref[:S])
-    Af_c, Bf_c = eng.jacobians(*_final_state(eng))
+    Af_c, Bf_c = eng.jacobians(x_f, u_f)
     A_f, B_f = _discrete(eng, Af_c[0], Bf_c[0])
     QT, _ = eng.dare_fixed_point(A_f, B_f, Q, R)
     K0 = eng.tv_lqr_gains(A_c, B_c, Q, R, QT, L=int(T_pred), nwin=n_steps, all_gains=False,

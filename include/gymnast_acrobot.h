@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 7
+#define GYM_ABI_VERSION 8
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -274,6 +274,16 @@ int gym_tv_lqr_gains(const double* A, const double* B, int32_t S, const double* 
  * did (the reference then prints "P_inf did not converge!!!" and returns the last P, :164-165). */
 int gym_dare_fixed_point(const double* A, const double* B, const double Q[16], const double R[4], int32_t max_iter,
                          double tol, double* P_out, int32_t* iters_out, void* stream);
+/* Fused MPC gains (solve_mpc_tracking :14-38 and every control step's QP, :43-49 / :73-140) in one launch:
+ * the discretised linearisation (Calculate_A_B_matrixes + discretize_linearization) of the reference's stages
+ * (x_ref (N,4), u_ref (N-1,2) [device], S = N-1 stages) and of the pad (A_f, B_f) at x_f (4), u_f (2) [device];
+ * Q_T = compute_P_inf(A_f, B_f, Q, R) (max_iter, tol as :144-165); the first gain of windows 0..nwin-1 of length
+ * L = T_pred (stage index >= S -> pad).  Replaces gym_dare_fixed_point + gym_tv_lqr_gains(discretize, !all_gains)
+ * on host-side Jacobians.  Outputs [device]: K_out (nwin,2,4), QT_out (4,4), iters_out (1) as
+ * gym_dare_fixed_point's.  Q, R [host].  2 <= L <= 254. */
+int gym_mpc_gains(const gym_model* m, const double* x_ref, const double* u_ref, int32_t S, const double* x_f,
+                  const double* u_f, const double Q[16], const double R[4], int32_t L, int32_t nwin, int32_t max_iter,
+                  double tol, double* K_out, double* QT_out, int32_t* iters_out, void* stream);
 /* solver_mpc's X_opt (L,4), U_opt (L-1,2): forward pass x_{s+1} = A_s x_s + B_s u_s, u_s = K_s x_s of one window
  * (gains from gym_tv_lqr_gains with all_gains), x0 (4) [device]. */
 int gym_lq_forward(const double* A, const double* B, int32_t S, const double* A_pad, const double* B_pad,
@@ -284,6 +294,13 @@ int gym_lq_forward(const double* A, const double* B, int32_t S, const double* A_
  * x0 (B,4); shared x_ff (N,4), u_ff (T,2), K (T,2,4); lane-major x_out (B,N,4), u_out (B,T,2). */
 int gym_track_rollout(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff, const double* K,
                       int64_t B, int32_t N, double* x_out, double* u_out, void* stream);
+/* gym_track_rollout with kernel selection: flags 0 = each trajectory on a lane pair (the default above: the
+ * joint-angle trigonometry of every RK4 step split between two lanes, DPP exchange; bit-identical results),
+ * GYM_TRACK_SINGLE = one lane per trajectory.  B <= 2^30. */
+#define GYM_TRACK_SINGLE 1
+int gym_track_rollout_ex(const gym_model* m, const double* x0, const double* x_ff, const double* u_ff,
+                         const double* K, int64_t B, int32_t N, int32_t flags, double* x_out, double* u_out,
+                         void* stream);
 
 /* [host] create / destroy the events of a gym_timing; collect = add the elapsed time of every pending
  * pair (call only after the stream that recorded them has been synchronised). */
