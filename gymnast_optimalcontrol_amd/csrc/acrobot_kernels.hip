@@ -1861,6 +1861,57 @@ __device__ __forceinline__ void run2_trial_main(ring_t ring, int lane, int64_t l
     lds_barrier(bw);
 }
 
+// the first Armijo trial's chain on a lane pair (GYM_RUN2_PAIR): two wavefronts share the 64 lanes' RK4 chains,
+// trajectory tl (< 64) of the workgroup on lanes (2q, 2q+1) of wavefront tl / 32 with q = tl % 32; the even lane
+// reduces / rotates th1, the odd lane th2 (gym::rk4_pair, bit-identical to rk4); the ring receives the same rows
+template <bool U0Z>
+__device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_t l, bool odd, int cb,
+                                                     unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    auto fetch = [&](TrialStage& q, int t) {
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        q.k0 = bld2(rK, o2, 0);
+        q.k1 = bld2(rK, o2, WROW);
+        q.cg = bld1(rsrc(Cb + (int64_t)t * row), o1, 0);
+    };
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    const int prow = odd ? 1 : 0;
+    auto step = [&](const TrialStage& q, int slot) {
+        const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
+        const KArgs ka = kernarg_consts();
+        gym::rk4_pair(ka.m, odd, n0, n1, n2, n3, v1, pk);
+        double2(*s)[BLK] = ring[slot];
+        s[prow][tl] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+        s[2][tl] = make_double2(v1, 0.0);   // both lanes of the pair: the same value
+    };
+    const int nch = run2_chunks(T);        // branch-free stream loads (see run2_sweep_helper)
+    TrialStage P[R2PD];
+#pragma unroll
+    for (int j = 0; j < R2PD; ++j) fetch(P[j], uni(min(j, T - 1)));
+    for (int c0 = 0; c0 < nch; c0 += R2PD / R2C) {
+#pragma unroll
+        for (int cc = 0; cc < R2PD / R2C; ++cc) {
+            const int c = c0 + cc;
+#pragma unroll
+            for (int j = 0; j < R2C; ++j) {
+                const int t = c * R2C + j, set = cc * R2C + j;
+                step(P[set], (c & 1) * R2C + j);
+                fetch(P[set], uni(min(t + R2PD, T - 1)));
+            }
+            lds_barrier(bw);
+        }
+    }
+    lds_barrier(bw);
+}
+
 // helper wavefront, first Armijo trial: u0, the running cost and the candidate's stores; returns J
 template <bool U0Z>
 __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64_t l, int cb, bool act,
@@ -1923,6 +1974,13 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
 #endif
 constexpr int R2H = GYM_RUN2_HELPERS;   // helper wavefronts: the sweep's stages are dealt to them round-robin
 static_assert(R2H == 1 || R2H == 2, "one or two helper wavefronts");
+#ifndef GYM_RUN2_PAIR
+#define GYM_RUN2_PAIR 1
+#endif
+// GYM_RUN2_PAIR: a further wavefront (index R2H + 1) joins the main one in the trial, each trajectory's RK4 chain
+// on a lane pair (run2_trial_main_pair); it idles through the sweep
+constexpr int R2P = GYM_RUN2_PAIR;
+constexpr int R2WAVES = 1 + R2H + R2P;
 
 // a helper wavefront that has no part in a pass still takes part in its chunk barriers
 __device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
@@ -1931,7 +1989,7 @@ __device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
 }
 
 template <bool U0Z>
-__global__ __launch_bounds__((1 + R2H) * BLK, 1) void k_nt_run2(RunArgs args) {
+__global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
     __shared__ double2 ring[R2S][R2W][BLK];
     __shared__ double shJ[BLK];
     __shared__ int shst[BLK];
@@ -1950,8 +2008,10 @@ __global__ __launch_bounds__((1 + R2H) * BLK, 1) void k_nt_run2(RunArgs args) {
         ++acc[3];
         if (wave == 1) {
             run2_sweep_helper<U0Z, 0, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
-        } else if (wave == 2) {
+        } else if (wave == 2 && R2H == 2) {
             run2_sweep_helper<U0Z, R2H - 1, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
+        } else if (wave > R2H) {
+            run2_idle(run_args()->N - 1, acc[4]);
         } else {
             double d, s;
             run2_sweep_main<U0Z>(ring, lane, l, cb, act, d, s, acc[4]);
@@ -1963,12 +2023,16 @@ __global__ __launch_bounds__((1 + R2H) * BLK, 1) void k_nt_run2(RunArgs args) {
             }
             lane_fence();                                  // K1 / cg visible to this wavefront's trial loads
         }
+        if (R2P) __syncthreads();                          // K1 / cg stored by the main wavefront, read by both
         acc[0] += R2T_NOW() - tt;
         tt = R2T_NOW();
         if (wave == 1) {
             shJ[lane] = run2_trial_helper<U0Z>(ring, lane, l, cb, act, run_args()->xr, run_args()->ur, acc[5]);
-        } else if (wave == 2) {
+        } else if (wave == 2 && R2H == 2) {
             run2_idle(run_args()->N - 1, acc[5]);
+        } else if (R2P) {                                  // wave 0 and wave R2H + 1: lane pairs
+            const int tl = (wave == 0 ? 0 : BLK / 2) + (lane >> 1);
+            run2_trial_main_pair<U0Z>(ring, tl, (int64_t)blockIdx.x * BLK + tl, lane & 1, cb, acc[5]);
         } else {
             run2_trial_main<U0Z>(ring, lane, l, cb, acc[5]);
         }
@@ -2548,7 +2612,7 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
         if (b->flags & GYM_FLAG_RUN_SINGLE)
             hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
         else   // two wavefronts per 64 lanes; every lane of the padded batch takes part (padding: GYM_PAD)
-            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3((1 + R2H) * BLK), 0, st, ra);
+            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3(R2WAVES * BLK), 0, st, ra);
     }
     // the statistics after iteration k1 - 1 ("lanes that ran" = the lanes that executed it; [4] = 0: this
     // schedule keeps no retry list)
