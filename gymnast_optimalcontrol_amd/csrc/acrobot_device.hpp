@@ -61,29 +61,33 @@ __device__ __forceinline__ PolyRegs poly_vgprs() {
 #ifndef GYM_HORNER_VOP3
 #define GYM_HORNER_VOP3 0
 #endif
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ double hfma(double z, double p, double c) {
-#if GYM_HORNER_VOP3
-    double r;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "v"(c));
-    return r;
-#else
-    return fma(z, p, c);
-#endif
+    if constexpr (V3) {
+        double r;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "v"(c));
+        return r;
+    } else {
+        return fma(z, p, c);
+    }
 }
 
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ double ksin(double r, double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(r * z, hfma(z, hfma(z, hfma(z, hfma(z, fma(z, k.s6, k.s5),
+    return fma(r * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.s6, k.s5),
         2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
         -1.66666666666666324348e-01), r);
 }
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ double kcos(double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(z * z, hfma(z, hfma(z, hfma(z, hfma(z, fma(z, k.c6, k.c5),
+    return fma(z * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.c6, k.c5),
         -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
         4.16666666666666019037e-02), fma(-0.5, z, 1.0));
 }
 
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ void fast_sincos(double x, double* s, double* c, const PolyRegs& k = poly_lits()) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     constexpr double kTwoOverPi = 6.36619772367581382433e-01;
@@ -93,8 +97,8 @@ __device__ __forceinline__ void fast_sincos(double x, double* s, double* c, cons
     const double qn = (fabs(kq) < 1048576.0) ? kq : __builtin_nan("");   // outside the domain: NaN
     const double r = fma(-qn, kPio2Lo, fma(-qn, kPio2Hi, x));
     const double z = r * r;
-    const double sr = ksin(r, z, k);
-    const double cr = kcos(z, k);
+    const double sr = ksin<V3>(r, z, k);
+    const double cr = kcos<V3>(z, k);
     const int q = (int)qn;                 // v_cvt_i32_f64 maps NaN to 0
     const double ss = (q & 1) ? cr : sr;   // quadrant rotation
     const double cc = (q & 1) ? sr : cr;
@@ -151,10 +155,11 @@ __device__ __forceinline__ void accel_sc(const Dyn& m, double s1, double c1, dou
 // rotation, ~20 VALU instead of ~40 for a reduction from scratch.  d = (h/2) w or h w is small; a lane
 // with |d| > pi/4 (|w| > 39 rad/s) reduces both arguments from scratch instead.  The choice is per lane,
 // so a lane's arithmetic never depends on which other lanes share its wavefront.
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ void rotate(double s, double c, double d, double& so, double& co, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
     const double z = d * d;
-    const double sd = ksin(d, z, k), cd = kcos(z, k);
+    const double sd = ksin<V3>(d, z, k), cd = kcos<V3>(z, k);
     so = fma(s, cd, c * sd);
     co = fma(c, cd, -(s * sd));
 }
@@ -220,6 +225,7 @@ __device__ __forceinline__ double pair_odd(double v) { return dpp_d<0xF5>(v); } 
 
 // substep_sincos() on a lane pair: this lane's angle tho (th1 on the even lane, th2 on the odd one), its
 // base sin/cos (so, co) and the angle increments d1, d2 of both joints (both lanes: the same branch)
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ void substep_sincos_pair(bool odd, double tho, double d1, double d2, double so, double co,
                                                     double& t1, double& u1, double& t2, double& u2,
                                                     const PolyRegs& k) {
@@ -227,14 +233,15 @@ __device__ __forceinline__ void substep_sincos_pair(bool odd, double tho, double
     const double d = odd ? d2 : d1;
     double to, uo;
     if (__builtin_expect(fabs(d1) <= kPio4 && fabs(d2) <= kPio4, 1)) {
-        rotate(so, co, d, to, uo, k);
+        rotate<V3>(so, co, d, to, uo, k);
     } else {   // also taken by NaN lanes
-        fast_sincos(tho + d, &to, &uo, k);
+        fast_sincos<V3>(tho + d, &to, &uo, k);
     }
     t1 = pair_even(to); u1 = pair_even(uo);
     t2 = pair_odd(to);  u2 = pair_odd(uo);
 }
 
+template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ void rk4_pair(const Dyn& m, bool odd, double& x0, double& x1, double& x2, double& x3,
                                          double tau2, const PolyRegs& k = poly_lits()) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
@@ -242,17 +249,17 @@ __device__ __forceinline__ void rk4_pair(const Dyn& m, bool odd, double& x0, dou
     double t1, u1, t2, u2;
     const double tho = odd ? x1 : x0;
     double so, co;
-    fast_sincos(tho, &so, &co, k);
+    fast_sincos<V3>(tho, &so, &co, k);
     const double s1 = pair_even(so), c1 = pair_even(co), s2 = pair_odd(so), c2 = pair_odd(co);
     accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
     const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
-    substep_sincos_pair(odd, tho, m.h2 * x2, m.h2 * x3, so, co, t1, u1, t2, u2, k);
+    substep_sincos_pair<V3>(odd, tho, m.h2 * x2, m.h2 * x3, so, co, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
     const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
-    substep_sincos_pair(odd, tho, m.h2 * y2, m.h2 * y3, so, co, t1, u1, t2, u2, k);
+    substep_sincos_pair<V3>(odd, tho, m.h2 * y2, m.h2 * y3, so, co, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
     const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
-    substep_sincos_pair(odd, tho, m.h * z2, m.h * z3, so, co, t1, u1, t2, u2, k);
+    substep_sincos_pair<V3>(odd, tho, m.h * z2, m.h * z3, so, co, t1, u1, t2, u2, k);
     accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
     const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
     const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;

@@ -1861,6 +1861,9 @@ __device__ __forceinline__ void run2_trial_main(ring_t ring, int lane, int64_t l
     lds_barrier(bw);
 }
 
+#ifndef GYM_RUN2_PAIR_VOP3
+#define GYM_RUN2_PAIR_VOP3 1   // three-address Horner steps in the pair trial (acrobot_device.hpp hfma)
+#endif
 // the first Armijo trial's chain on a lane pair (GYM_RUN2_PAIR): two wavefronts share the 64 lanes' RK4 chains,
 // trajectory tl (< 64) of the workgroup on lanes (2q, 2q+1) of wavefront tl / 32 with q = tl % 32; the even lane
 // reduces / rotates th1, the odd lane th2 (gym::rk4_pair, bit-identical to rk4); the ring receives the same rows
@@ -1887,7 +1890,7 @@ __device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_
     auto step = [&](const TrialStage& q, int slot) {
         const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
         const KArgs ka = kernarg_consts();
-        gym::rk4_pair(ka.m, odd, n0, n1, n2, n3, v1, pk);
+        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, v1, pk);
         double2(*s)[BLK] = ring[slot];
         s[prow][tl] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
         s[2][tl] = make_double2(v1, 0.0);   // both lanes of the pair: the same value
