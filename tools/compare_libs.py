@@ -24,7 +24,8 @@ def run(lib, a, x0):
     x_ref, u_ref = load_refs()
     eng = AcrobotEngine(lib_path=os.path.abspath(lib))
     s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1,
-                            pipeline={"serial": False, "pipelined": True}[a.schedule])
+                            pipeline={"serial": False, "pipelined": True, "persistent": False}[a.schedule],
+                            persistent=a.schedule == "persistent")
     s.max_iters = a.iters
     s.init(x0)
     for _ in range(a.iters):
@@ -41,7 +42,7 @@ def main():
     ap.add_argument("lib_b")
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--schedule", choices=("serial", "pipelined"), default="serial")
+    ap.add_argument("--schedule", choices=("serial", "pipelined", "persistent"), default="serial")
     a = ap.parse_args()
     from bench import make_x0
     x0 = make_x0(a.batch)
