@@ -52,6 +52,50 @@ def test_cfg2_full_size_matches_c_oracle():
     assert rel_l2(r.x[0].cpu().numpy(), g["x"]) < TOL_TRAJ and rel_l2(r.u[0].cpu().numpy(), g["u"]) < TOL_TRAJ
 
 
+# ----------------------------------------------------------------------------- BASELINE cfg 4 (one GPU)
+def test_cfg4_global_batch_on_one_gpu():
+    """BASELINE cfg 4's whole batch, 1,048,576 lanes (bench.py's strong-scaling workload at N = 1; the pipelined
+    schedule), solved to convergence on one GPU, checked through size-independent properties: every lane
+    converges; lanes 0..4095 (make_x0 draws the same rows for any batch size) are bit for bit the cfg 2 solve of
+    those 4,096 lanes (persistent schedule: per-lane results do not depend on the batch, its size or the
+    schedule); 64 lanes spread over the batch match the C oracle's decisions and trajectories; lane 0 the
+    reference's npz."""
+    import torch
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from oracle import c_oracle
+    x_ref, u_ref = load_refs()
+    B = 1 << 20
+    x0 = make_x0(B)
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20)
+    s = BatchedNewtonSolver(eng, x_ref, u_ref, B, **kw)
+    assert s.schedule == "pipelined"
+    r = s.solve(x0, 5000, sync_every=4)
+    st = r.status.cpu().numpy()
+    assert (st == 1).all(), np.bincount(st)
+    ni = r.n_iter.cpu().numpy()
+    head = {k: getattr(r, k)[:4096].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")}
+    head["n_iter"], head["n_roll"] = ni[:4096], r.n_rollouts[:4096].cpu().numpy()
+    pick = np.linspace(0, B - 1, 64).astype(np.int64)
+    xs, us = r.x[pick].cpu().numpy(), r.u[pick].cpu().numpy()
+    x0l, u0l = r.x[0].cpu().numpy(), r.u[0].cpu().numpy()
+    del r, s
+    torch.cuda.empty_cache()
+    g = load_golden("task2_reference_output")
+    assert rel_l2(x0l, g["x"]) < TOL_TRAJ and rel_l2(u0l, g["u"]) < TOL_TRAJ
+    o = c_oracle.newton_solve(x0[pick], x_ref, u_ref, max_iters=5000, tol=1e-4, gamma_0=0.1)
+    np.testing.assert_array_equal(ni[pick], o["n_iter"])
+    assert _lane_rel(xs, o["x"]).max() < TOL_TRAJ and _lane_rel(us, o["u"]).max() < TOL_TRAJ
+    r2 = BatchedNewtonSolver(eng, x_ref, u_ref, 4096, **kw).solve(x0[:4096], 5000)
+    assert r2.schedule == "persistent"
+    np.testing.assert_array_equal(head["n_iter"], r2.n_iter.cpu().numpy())
+    np.testing.assert_array_equal(head["n_roll"], r2.n_rollouts.cpu().numpy())
+    for k in ("x", "u", "K", "sigma", "cost"):
+        np.testing.assert_array_equal(head[k], getattr(r2, k).cpu().numpy(), err_msg=k)
+
+
 # ----------------------------------------------------------------------------- BASELINE cfg 5
 def test_cfg5_full_size_matches_oracle():
     """BASELINE cfg 5 exactly as bench.py --workload mpc runs it: 8,192 disturbed initial states, horizon 50,
