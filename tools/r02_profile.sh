@@ -25,6 +25,10 @@ for s in "$@"; do
     fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" ;;
     write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" ;;
     valu)  run pmc_valu 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_nt_" -d $OUT/pmc_valu -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" ;;
+    fetch2) run pmc_fetch_cfg2 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_nt_run" -d $OUT/pmc_fetch_cfg2 -o run --output-format csv -- python3 bench.py --batch 4096 --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" ;;
+    write2) run pmc_write_cfg2 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_run" -d $OUT/pmc_write_cfg2 -o run --output-format csv -- python3 bench.py --batch 4096 --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" ;;
+    fetchm) run pmc_fetch_mpc 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_track|k_mpc" -d $OUT/pmc_fetch_mpc -o run --output-format csv -- python3 bench.py --workload mpc --steps 2 --warmup 1 ;;
+    writem) run pmc_write_mpc 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_track|k_mpc" -d $OUT/pmc_write_mpc -o run --output-format csv -- python3 bench.py --workload mpc --steps 2 --warmup 1 ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --tb=short --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench_default 900 python -u bench.py ;;
