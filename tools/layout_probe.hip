@@ -8,6 +8,7 @@
 //   soa   : today's (t, row, lane) -- a wave's rows of one stage are Bp*16 bytes apart
 //   wb    : wave-blocked (t, wave, row, lane%64) -- a wave's rows of one stage are one contiguous block
 //   wbm   : wb with K1 and cs merged into one 3-row stream (one 3 KiB block per wave-stage)
+//   aos   : AoSoA (wave, t, row, lane%64) -- a wave's stages of a stream are one contiguous region (planes too)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/layout_probe.hip -o tools/layout_probe
 #include <hip/hip_runtime.h>
 
@@ -33,14 +34,22 @@ __device__ __forceinline__ void st2(double2* p, double a, double b) {
     __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(p));
 }
 
-enum { SOA = 0, WB = 1, WBM = 2 };
+enum { SOA = 0, WB = 1, WBM = 2, AOS = 3 };
+constexpr int kTn = 501;   // AOS: stages per wave region (N for every stream; the probe pads the T-stage ones)
 
 // element index (double2 units) of row p of a P-row stream at stage t for lane l
 template <int L>
 __device__ __forceinline__ long long ix(int t, int p, int P, long long l, long long B) {
     if (L == SOA) return ((long long)t * P + p) * B + l;
+    if (L == AOS) return (((l >> 6) * kTn + t) * P + p) * 64 + (l & 63);
     const long long w = l >> 6, q = l & 63, nW = B >> 6;
     return (((long long)t * nW + w) * P + p) * 64 + q;
+}
+
+template <int L>   // plane element (double units) of stage t, lane l
+__device__ __forceinline__ long long px(int t, long long l, long long B) {
+    if (L == AOS) return ((l >> 6) * kTn + t) * 64 + (l & 63);
+    return (long long)t * B + l;
 }
 
 template <int L>
@@ -50,7 +59,7 @@ __device__ __forceinline__ void sweep_lane(const double2* __restrict__ x, const 
     double p0 = 1.0, p1 = 2.0;
     for (int t = T - 1; t >= 0; --t) {
         const double2 xa = ld2(&x[ix<L>(t, 0, 2, l, B)]), xb = ld2(&x[ix<L>(t, 1, 2, l, B)]);
-        const double uu = __builtin_nontemporal_load(&u1[(long long)t * B + l]);
+        const double uu = __builtin_nontemporal_load(&u1[px<L>(t, l, B)]);
         p0 = 0.5 * p0 + xa.x * xb.y + uu;
         p1 = 0.5 * p1 + xa.y * xb.x;
         if (L == WBM) {
@@ -80,7 +89,7 @@ __device__ __forceinline__ void trial_lane(const double2* __restrict__ K, const 
         const double v = c.x + a0 * k0.x + a1 * k0.y + a2 * k1.x + a3 * k1.y + c.y;
         acc += v;
         a0 += 1e-3 * v; a1 -= 1e-3 * v; a2 += 1e-4 * c.x; a3 += 1e-4 * c.y;
-        __builtin_nontemporal_store(v, &u1[(long long)t * B + l]);
+        __builtin_nontemporal_store(v, &u1[px<L>(t, l, B)]);
         st2(&xn[ix<L>(t + 1, 0, 2, l, B)], a0, a1);
         st2(&xn[ix<L>(t + 1, 1, 2, l, B)], a2, a3);
     }
@@ -109,7 +118,7 @@ __global__ __launch_bounds__(64, 4) void k_phase(const double2* x0, const double
 int main(int argc, char** argv) {
     const long long B = argc > 1 ? atoll(argv[1]) : 262144;
     const int N = 501, T = N - 1, reps = 5;
-    const size_t xs = (size_t)N * 2 * B, ks = (size_t)T * 3 * B, us = (size_t)T * B;
+    const size_t xs = (size_t)N * 2 * B, ks = (size_t)N * 3 * B, us = (size_t)N * B;
     double2 *x, *xn, *K, *cs;
     double *u, *un, *sink;
     CK(hipMalloc(&x, xs * 16)); CK(hipMalloc(&xn, xs * 16)); CK(hipMalloc(&K, ks * 16)); CK(hipMalloc(&cs, us * 16));
@@ -142,10 +151,12 @@ int main(int argc, char** argv) {
     timeit("sweep_" NAME, [&] { hipLaunchKernelGGL(k_sweep<L>, dim3(g), dim3(64), 0, 0, x, u, K, cs, B, T); });       \
     timeit("trial_" NAME, [&] { hipLaunchKernelGGL(k_trial<L>, dim3(g), dim3(64), 0, 0, K, cs, xn, un, B, T, sink); }); \
     timeit("phase_" NAME, [&] { hipLaunchKernelGGL(k_phase<L>, dim3(g), dim3(64), 0, 0, x, u, K, cs, xn, un, B, T, sink); });
-    for (int pass = 0; pass < 2; ++pass) {
-        RUN3(SOA, "soa")
+    const bool all = argc > 2 && atoi(argv[2]);
+    for (int pass = 0; pass < 3; ++pass) {
+        if (all) { RUN3(SOA, "soa") }
         RUN3(WB, "wb")
-        RUN3(WBM, "wbm")
+        RUN3(AOS, "aos")
+        if (all) { RUN3(WBM, "wbm") }
     }
     CK(hipGetLastError());
     return 0;
