@@ -178,7 +178,8 @@ __global__ __launch_bounds__(64) void k_dare_fixed_point(const double* __restric
 //
 // Lane-parallel map: a 16-lane group evaluates one map; lane 4i+j owns P[i][j] and the (i, j) entry of every
 // product.  Row i of P comes from the lane's own quad (DPP quad broadcasts); rows 2, 3 and i&1 of PA and PB
-// come from the group's other quads through ds_swizzle (no LDS storage, no barrier).  A map is then ~35 fp64
+// come from the group's other quads: the PB rows (uniform in a quad, on the gain's critical path) through
+// row broadcasts (one v_mov_b64_dpp each), the PA rows through ds_swizzle (no LDS storage, no barrier).  A map is then ~35 fp64
 // instructions per lane and a handful of exchanges on the critical path, instead of ~400 dependent flops of one
 // lane (k_tv_lqr_gains) or three LDS round trips with barriers (k_dare_fixed_point).
 // ------------------------------------------------------------------------------------------
@@ -201,6 +202,11 @@ __device__ __forceinline__ void disc_stage(const Dyn& m, double x0, double x1, d
 }
 
 using gym::dpp_d;
+template <int N>   // v_mov_b64_dpp row_newbcast:N -- lane N of each 16-lane row to the whole row (gfx90a+ DPP64)
+__device__ __forceinline__ double bcast_d(double v) {
+    return __longlong_as_double(
+        __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(v), 0x150 + N, 0xF, 0xF, false));
+}
 template <int AND, int OR>   // ds_swizzle bit mode inside 32-lane halves: lane' = (lane & AND) | OR
 __device__ __forceinline__ double swz_d(double v) {
     constexpr int pat = (AND & 31) | ((OR & 31) << 5);
@@ -212,12 +218,14 @@ __device__ __forceinline__ double swz_d(double v) {
 
 // per-lane constants of the map: lane 4i+j of its group
 struct MapLane {
+    bool hi;           // i & 1
     double c0j, c1j;   // A_d[0][j], A_d[1][j]
     double ci;         // A_d[0][i] + A_d[1][i] (exactly one of the two is nonzero): 1, 1, h, h
     double Qij, R00, R01, R10, R11;
 };
 __device__ __forceinline__ MapLane map_lane(int i, int j, double h, const M44& Q, const M22& R) {
     MapLane c;
+    c.hi = i & 1;
     c.c0j = j == 0 ? 1.0 : (j == 2 ? h : 0.0);
     c.c1j = j == 1 ? 1.0 : (j == 3 ? h : 0.0);
     c.ci = i < 2 ? 1.0 : h;
@@ -234,13 +242,14 @@ __device__ __forceinline__ double riccati_map_lane(double P, const MapLane& c, d
     // the gain's critical path is P -> PB -> aux1 -> 1/det -> K: PB and its exchanges are issued first
     const double P2 = dpp_d<0xAA>(P), P3 = dpp_d<0xFF>(P);                    // P[i][2], P[i][3]
     const double PB = P2 * b2 + P3 * b3;                                      // (PB)[i][1]; (PB)[i][0] = 0
-    const double PB2 = swz_d<0x10, 0x08>(PB), PB3 = swz_d<0x10, 0x0C>(PB);
+    const double PB2 = bcast_d<8>(PB), PB3 = bcast_d<12>(PB);                 // (PB)[2][1], (PB)[3][1]
     const double P0 = dpp_d<0x00>(P), P1 = dpp_d<0x55>(P);
     const double PA = ((P0 * c.c0j + P1 * c.c1j) + P2 * a2j) + P3 * a3j;     // (PA)[i][j]
     const double a1 = c.R11 + (b2 * PB2 + b3 * PB3);                           // aux1[1][1]; aux1[0][*] = R[0][*]
     const double idet = gym::recip(c.R00 * a1 - c.R01 * c.R10);              // rcp + 2 Newton steps
     const double PA2 = swz_d<0x13, 0x08>(PA), PA3 = swz_d<0x13, 0x0C>(PA), PAh = swz_d<0x17, 0x00>(PA);
-    const double PBh = swz_d<0x14, 0x00>(PB);
+    const double B0 = bcast_d<0>(PB), B4 = bcast_d<4>(PB);
+    const double PBh = c.hi ? B4 : B0;                                        // (PB)[i&1][1]
     const double a2 = b2 * PA2 + b3 * PA3;                                    // aux2[1][j]; aux2[0][j] = 0
     K0j = -((-c.R01 * idet) * a2);                                            // -(inv(aux1) aux2)[0][j]
     K1j = -((c.R00 * idet) * a2);                                             // -(inv(aux1) aux2)[1][j]
