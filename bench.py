@@ -65,9 +65,11 @@ def load_refs():
     return d["x"], 2.0 * u_ref          # get_fully_actuated_ref (trajectory_generation.py:511-518)
 
 
-def make_x0(total: int, seed: int = 0) -> np.ndarray:
+def make_x0(total: int, seed: int = 0, spread: float = 0.5) -> np.ndarray:
+    """x0 = [th1, th2, 0, 0], th ~ U(-spread, spread) from default_rng(seed) (spread 1.5 is its stress
+    variant); lane 0 = 0."""
     x0 = np.zeros((total, 4))
-    x0[:, :2] = np.random.default_rng(seed).uniform(-0.5, 0.5, (total, 2))
+    x0[:, :2] = np.random.default_rng(seed).uniform(-spread, spread, (total, 2))
     x0[0] = 0.0                          # golden lane (main.task_2, main.py:55)
     return x0
 
@@ -179,7 +181,7 @@ class NewtonLeg:
         from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
         self.rank, self.world = gd.rank_world()
         self.total = int(total)
-        self.x0_all = make_x0(self.total)
+        self.x0_all = make_x0(self.total, spread=a.spread)
         lo, hi = gd.shard_range(self.total, self.rank, self.world)
         sched = {"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule]
         self.solver = BatchedNewtonSolver(
@@ -202,17 +204,19 @@ class NewtonLeg:
         gd.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        lane_its, res = 0, None
+        lane_its, rolls, res = 0, 0, None
         for _ in range(steps):
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
             lane_its += res.lane_iterations
+            rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
         torch.cuda.synchronize()
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
         self.res, self.lane_its, self.steps = res, lane_its, steps
         self.elapsed = elapsed
         self.lane_its_all = int(gd.sum_over_ranks(lane_its))
+        self.rollouts_all = int(gd.sum_over_ranks(rolls))
         self.value = self.lane_its_all / elapsed
         return self
 
@@ -263,8 +267,7 @@ class NewtonLeg:
         return kern, roof
 
     def schedule(self) -> str:
-        s = self.solver
-        return "persistent" if s.persistent else ("pipelined" if s.pipeline else "serial")
+        return self.res.schedule if self.res is not None else self.solver.schedule
 
     def free(self):
         import torch
@@ -312,9 +315,10 @@ def main():
     ap.add_argument("--sync-every", type=int, default=4,
                     help="outer iterations between host reads of the (all-reduced) statistics; iterations "
                          "enqueued after every lane has finished are no-ops")
-    ap.add_argument("--workload", choices=("newton", "cfg4", "mpc"), default="newton",
+    ap.add_argument("--workload", choices=("newton", "cfg4", "mpc", "stress"), default="newton",
                     help="newton: the north-star metric (cfg 3 per GPU, weak scaling); cfg4: 1,048,576 lanes "
-                         "strong-scaled over the ranks; mpc: BASELINE cfg 5")
+                         "strong-scaled over the ranks; mpc: BASELINE cfg 5; stress: the cfg 3 batch with "
+                         "th ~ U(+-1.5) (SURVEY 8(d)'s stress variant: backtracking and Armijo failures)")
     ap.add_argument("--extra-legs", default="cfg4,general",
                     help="comma list of secondary timed legs reported inside the same JSON line (newton "
                          "workload): cfg4 = 1,048,576 lanes strong-scaled over the ranks; general = the same "
@@ -336,6 +340,7 @@ def main():
         return run_mpc(a)
     if a.workload == "cfg4" and a.global_batch is None:
         a.global_batch = CFG4_LANES
+    a.spread = 1.5 if a.workload == "stress" else 0.5
 
     import torch
     from gymnast_optimalcontrol_amd import distributed as gd
@@ -370,11 +375,20 @@ def main():
                   "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())],
                   "rollouts": int(res.n_rollouts.sum().item()),
                   "lanes_that_backtracked": int((res.n_rollouts > res.n_iter).sum().item())}
+        # per-lane extra Armijo trials over the solve (rollouts beyond one per iteration), binned
+        extra = (res.n_rollouts - res.n_iter).cpu().numpy()
+        edges = [0, 1, 2, 4, 8, 16, 32, 1 << 30]
+        parity["extra_trials_histogram"] = {
+            (f"{lo}" if hi == lo + 1 else f"{lo}-{hi - 1}" if hi < (1 << 30) else f">={lo}"): int(((extra >= lo) & (extra < hi)).sum())
+            for lo, hi in zip(edges[:-1], edges[1:])}
 
     per_gpu = -(-total // world)
     if strong:
         label = (f"{'cfg4' if total == CFG4_LANES else 'custom'}: {total} randomised-theta0 acrobot swing-ups "
                  f"strong-scaled over {world} GPU(s) ({per_gpu} per GPU)")
+    elif a.workload == "stress":
+        label = (f"stress (SURVEY 8(d)): {a.batch} acrobot swing-ups per GPU, theta0 ~ U(+-1.5) (backtracking and "
+                 f"Armijo failures)" + (f" x {world} GPUs (weak scaling)" if world > 1 else ""))
     else:
         label = (f"{ {4096: 'cfg2', 262144: 'cfg3'}.get(a.batch, 'custom') }: {a.batch} randomised-theta0 acrobot "
                  f"swing-ups per GPU" + (f" x {world} GPUs (weak scaling)" if world > 1 else ""))
@@ -385,6 +399,7 @@ def main():
                       "lanes_per_gpu": per_gpu, "global_lanes": total, "horizon_T": T,
                       "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats per host sync)"},
            "states_per_s": value * T}
+    out["rollouts_per_s"] = main_leg.rollouts_all / main_leg.elapsed   # closed-loop Armijo rollouts, all ranks
 
     kern, roof = main_leg.kernel_report(N)
     if kern and rank == 0:
@@ -434,7 +449,7 @@ def main():
         leg.free()
 
     if rank == 0 and world == 1 and not a.no_cpu:
-        x0_all = make_x0(total)
+        x0_all = make_x0(total, spread=a.spread)
         out["cpu_baseline"] = cpu_baseline(x0_all, x_ref, u_ref, a.cpu_lanes, a.max_iters)
         out["cpu_baseline"]["numpy"] = numpy_baseline(x0_all, x_ref, u_ref, a.numpy_lanes, a.numpy_iters)
         out["cpu_baseline"]["reference_python_single_core"] = {
