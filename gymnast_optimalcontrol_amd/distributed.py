@@ -102,13 +102,15 @@ def sum_over_ranks(value: float, group=None) -> float:
     return float(t.item())
 
 
-def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool = False, **solver_kw):
+def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool = False, gather: bool = False,
+                  **solver_kw):
     """Solve this rank's contiguous shard of ``x0_all`` (B_total,4); stop on the GLOBAL active count.
 
     Every rank must hold a non-empty shard (``len(x0_all) >= world``; checked on every rank before any
     collective, so all of them raise together).  The automatic schedule is chosen on the largest shard
     (``schedule_lanes``), so every rank runs the same schedule and issues its all-reduces at the same
-    iterations.  Returns (lo, hi, SolveResult of the local shard)."""
+    iterations.  Returns (lo, hi, SolveResult of the local shard); with ``gather=True`` the third item is instead
+    the dict of global per-lane results (``gather_sharded`` of GATHER_FIELDS) on every rank."""
     from .engine import AcrobotEngine
     from .solver import BatchedNewtonSolver
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -121,7 +123,37 @@ def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool
     solver_kw.setdefault("schedule_lanes", schedule_lanes(total, world))
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **solver_kw)
     res = solver.solve(np.asarray(x0_all)[lo:hi], max_iters, reduce_stats=make_reduce_stats(), keep_stats=keep_stats)
+    if gather:
+        return lo, hi, gather_sharded({f: getattr(res, f) for f in GATHER_FIELDS}, total)
     return lo, hi, res
+
+
+GATHER_FIELDS = ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma")
+
+
+def gather_sharded(local: dict, total: int, group=None) -> dict:
+    """The global per-lane results on every rank from each rank's contiguous shard ("ship the final
+    per-lane outputs with an all-gather ... only if requested"): ``local`` maps a name to this rank's
+    (hi - lo, ...) tensor; returns name -> (total, ...) tensors in lane order.  Ragged shards are padded to the
+    largest one for the collective (RCCL all-gather on device tensors; gloo moves them through the host)."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return dict(local)
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    lo, hi = shard_range(total, rank, world)
+    width = -(-int(total) // world)
+    gloo = dist.get_backend(group) == "gloo"
+    out = {}
+    for name, t in local.items():
+        if t.shape[0] != hi - lo:
+            raise ValueError(f"{name}: {t.shape[0]} rows for the shard [{lo}, {hi})")
+        src = t.detach().cpu() if gloo else t.detach()
+        pad = torch.zeros((width,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        pad[:hi - lo] = src
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        rows = [parts[r][:shard_range(total, r, world)[1] - shard_range(total, r, world)[0]] for r in range(world)]
+        out[name] = torch.cat(rows).to(t.device)
+    return out
 
 
 def schedule_lanes(total: int, world: int) -> int:

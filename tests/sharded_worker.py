@@ -23,6 +23,8 @@ def main():
     x0 = sharded_x0(total, seed)
     lo, hi, res = gd.solve_sharded(x0, x_ref, u_ref, max_iters, keep_stats=True, tol=1e-4, gamma_0=0.1)
     import torch.distributed as dist
+    g = gd.gather_sharded({"cost": res.cost, "n_iter": res.n_iter, "status": res.status}, total)
+    np.savez(f"{out}.gathered.rank{rank}.npz", **{k: v.cpu().numpy() for k, v in g.items()})
     np.savez(f"{out}.rank{rank}.npz", lo=lo, hi=hi, x=res.x.cpu().numpy(), u=res.u.cpu().numpy(),
              K=res.K.cpu().numpy(), sigma=res.sigma.cpu().numpy(), cost=res.cost.cpu().numpy(),
              n_iter=res.n_iter.cpu().numpy(), status=res.status.cpu().numpy(),

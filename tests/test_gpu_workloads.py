@@ -229,6 +229,10 @@ def test_sharded_solve_on_hip_matches_unsharded(total, tmp_path):
     r = s.solve(x0, max_iters)
     full = {k: getattr(r, k).cpu().numpy() for k in ("x", "u", "K", "sigma", "cost", "n_iter", "status",
                                                       "n_rollouts")}
+    for rk in range(2):                  # distributed.gather_sharded: the global per-lane results on every rank
+        g = np.load(f"{out}.gathered.rank{rk}.npz")
+        for k in ("cost", "n_iter", "status"):
+            np.testing.assert_array_equal(g[k], full[k], err_msg=f"gathered {k} on rank {rk}")
     for p_ in parts:
         lo, hi = int(p_["lo"]), int(p_["hi"])
         for k, v in full.items():
