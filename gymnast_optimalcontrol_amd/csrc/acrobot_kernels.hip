@@ -170,6 +170,13 @@ __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "
 
 // element index of (t, row p of P, lane) in a time-major plane stream (W = 1 doubles): (L, P, Bp)
 __device__ __forceinline__ int64_t pix(int t, int p, int P, int64_t l, int64_t Bp) { return ((int64_t)t * P + p) * Bp + l; }
+// Per-lane references (GYM_FLAG_REF_LANE, the serial schedule): x_ref (Bp, N, 4), u_ref (Bp, T, 2), lane-major.
+// RL kernels offset the reference pointers by the lane once; everything downstream reads stage t at +4t / +2t as
+// with the shared reference (then by vector instead of scalar loads: the same values, the same bits).
+template <bool RL>
+__device__ __forceinline__ const double* lane_ref(const double* r, int64_t l, int64_t per_lane) {
+    return RL ? r + l * per_lane : r;
+}
 // element index of (t, row p of P, lane) in a wave-blocked pair stream (W = 2, double2): (L, Bp/64, P, 64), i.e.
 // the P rows of one wavefront's 64 lanes at one stage form one contiguous P KiB block (one DRAM burst sequence
 // instead of P 1-KiB pieces Bp*16 bytes apart).  The stage stride is P*Bp elements, as for planes.
@@ -1108,12 +1115,13 @@ struct SrcSigma {   // sigma of each lane's last iteration: sigma0 recomputed fr
     KW w;
     const double *cs, *u0b, *u1b, *ur;
     const int32_t* n_iter;
+    int64_t ur_lane;   // per-lane references: doubles per lane of u_ref (0: shared)
     __device__ __forceinline__ double operator()(int64_t t, int c, int64_t lane, int64_t Bp) const {
         const int it = n_iter[lane];
         if (it <= 0) return 0.0;
         if (c == 1) return cs[pix((int)t, 1, 2, lane, Bp)];
         const double* u = ((it - 1) & 1) ? u1b : u0b;
-        return -(w.G00 * (u[pix((int)t, 0, 2, lane, Bp)] - ur[2 * t])) * w.iG00;
+        return -(w.G00 * (u[pix((int)t, 0, 2, lane, Bp)] - ur[lane * ur_lane + 2 * t])) * w.iG00;
     }
 };
 
@@ -1160,6 +1168,7 @@ __global__ __launch_bounds__(TILE_THREADS) void k_unpack_tiled(Src src, double* 
 // ------------------------------------------------------------------------------------------
 // kernels: batched Newton / Armijo solver (newton_Algorithm :298-398)
 // ------------------------------------------------------------------------------------------
+template <bool RL = false>
 __global__ __launch_bounds__(BLK) void k_init(Dyn m, KW w, const double* __restrict__ x0,
                                               const double* __restrict__ u, const double* __restrict__ xr,
                                               const double* __restrict__ ur, double2* __restrict__ xn,
@@ -1177,7 +1186,8 @@ __global__ __launch_bounds__(BLK) void k_init(Dyn m, KW w, const double* __restr
         return;
     }
     status[l] = GYM_ACTIVE;
-    cost[l] = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, xr, ur, xn, nullptr, 0.0, l, Bp, N,
+    cost[l] = rollout_ref<false>(m, w, nullptr, u, nullptr, nullptr, lane_ref<RL>(xr, l, 4 * (int64_t)N),
+                                 lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), xn, nullptr, 0.0, l, Bp, N,
                                  x0[4 * l + 0], x0[4 * l + 1], x0[4 * l + 2], x0[4 * l + 3]);
 }
 
@@ -1243,13 +1253,15 @@ __device__ __forceinline__ void backward_solver(const Dyn& m, const KW& w, const
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;                                          \
     GYM_CK_LDS(CK, U0Z);                                                                                        \
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;                                                          \
-    backward_solver<U0Z, CK, OUT>(m, w, x, u, xr, ur, K1, cs, g0, dJ, smax, hist_smax, l, Bp, N, k, hist_len, ck_lds);
+    backward_solver<U0Z, CK, OUT>(m, w, x, u, lane_ref<RL>(xr, l, 4 * (int64_t)N),                               \
+                                  lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), K1, cs, g0, dJ, smax, hist_smax, l, Bp, \
+                                  N, k, hist_len, ck_lds);
 
 // the solver's serial-schedule sweep (K1, cg) ...
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK, 4) void k_nt_backward(GYM_NT_BACKWARD_PARAMS) { GYM_NT_BACKWARD_BODY(OUT_SOLVER) }
 // ... and the same sweep also storing sigma1, for the gamma sweeps of gym_newton_gamma_sweep
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK, 4) void k_nt_backward_all(GYM_NT_BACKWARD_PARAMS) { GYM_NT_BACKWARD_BODY(OUT_ALL) }
 
 struct SolverCtl {
@@ -1309,7 +1321,7 @@ __device__ __forceinline__ void trial_solver(const Dyn& m, const KW& w, const So
     }
 }
 
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK, 4) void k_nt_trial(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                      const double2* __restrict__ K1, const double* __restrict__ cs,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
@@ -1322,7 +1334,8 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_trial(Dyn m, KW w, SolverCtl a, T
     const int64_t l = rg.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= rg.hi || status[l] != GYM_ACTIVE) return;
     GYM_TRACE_WAVE(1);
-    trial_solver<U0Z, CK>(m, w, a, io, K1, cs, xr, ur, cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
+    trial_solver<U0Z, CK>(m, w, a, io, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N), lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)),
+                          cost, dJ, smax, gamma, status, n_iter, res_buf, n_roll,
                       retry_list + rg.lo, counter, hist_cost, l, Bp, N);
 }
 
@@ -1408,7 +1421,7 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
 }
 
 // Armijo trials 2..max_ls evaluated in parallel: one thread per (lane, j), cost only.
-template <bool U0Z>
+template <bool U0Z, bool RL = false>
 __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                        const double2* __restrict__ K1, const double* __restrict__ cs,
                                                        const double* __restrict__ xr, const double* __restrict__ ur,
@@ -1425,14 +1438,15 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a,
         double g = a.gamma0;
         for (int q = 0; q < j; ++q) g *= a.beta;  // gamma_i *= beta, sequentially (:365)
         const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
-        const double Jn = rollout_cform<false, U0Z, true>(m, w, io.u, K1, cs, xr, ur, nullptr, nullptr, g, a.gamma0, l,
-                                                          Bp, N, xa.x, xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<false, U0Z, true>(m, w, io.u, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N),
+                                                          lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), nullptr, nullptr,
+                                                          g, a.gamma0, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
         cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
     }
 }
 
 // First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                   const double2* __restrict__ K1, const double* __restrict__ cs,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
@@ -1460,8 +1474,9 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
         const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
-        const double Jn = rollout_cform<true, U0Z, true, CK>(m, w, io.u, K1, cs, xr, ur, io.xn, io.un, g, a.gamma0, l,
-                                                             Bp, N, xa.x, xa.y, xb.x, xb.y);
+        const double Jn = rollout_cform<true, U0Z, true, CK>(m, w, io.u, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N),
+                                                             lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), io.xn, io.un, g,
+                                                             a.gamma0, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -2222,7 +2237,7 @@ __global__ __launch_bounds__(64 * NSTAT) void k_stats_final(const double* __rest
 // sigma1 plane.  retry mode (list != nullptr): the lanes list[0 .. *count) at the iterate (x, u); final mode:
 // the lanes whose last iteration started from this buffer, (n_iter - 1) & 1 == parity (one launch per
 // buffer, so the streams' base addresses stay wave-uniform).
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK, 4) void k_nt_sigma(Dyn m, KW w, const double2* __restrict__ x,
                                                      const double* __restrict__ u, const double* __restrict__ xr,
                                                      const double* __restrict__ ur, double* __restrict__ cs,
@@ -2237,8 +2252,9 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_sigma(Dyn m, KW w, const double2*
             const int it = n_iter[l];
             if (it <= 0 || ((it - 1) & 1) != parity) continue;
         }
-        backward_solver<U0Z, CK, OUT_SIGMA>(m, w, x, u, xr, ur, nullptr, cs, 0.0, nullptr, nullptr, nullptr, l, Bp, N,
-                                            0, 0, ck_lds);
+        backward_solver<U0Z, CK, OUT_SIGMA>(m, w, x, u, lane_ref<RL>(xr, l, 4 * (int64_t)N),
+                                            lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), nullptr, cs, 0.0, nullptr,
+                                            nullptr, nullptr, l, Bp, N, 0, 0, ck_lds);
     }
 }
 
@@ -2296,6 +2312,15 @@ struct TimedLaunch {  // records a start/stop event pair around one launch if th
 #define SOLVER_SEL(b, kern)                                                                               \
     (((b)->flags & GYM_FLAG_U0_ZERO) ? (((b)->flags & GYM_FLAG_X_CKPT) ? kern<true, true> : kern<true, false>) \
                                      : (((b)->flags & GYM_FLAG_X_CKPT) ? kern<false, true> : kern<false, false>))
+
+// ... and, for the serial schedule's kernels, per-lane references (GYM_FLAG_REF_LANE; never with X_CKPT)
+#define SERIAL_SEL(b, kern)                                                                                      \
+    (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false, true>              \
+                                                                          : kern<false, false, true>)           \
+                                      : SOLVER_SEL(b, kern))
+#define CAND_SEL(b, kern)                                                                                        \
+    (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, true> : kern<false, true>) \
+                                      : (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false> : kern<false, false>))
 
 inline bool bad_dims(int64_t B, int64_t Bp, int N) {
     return B <= 0 || Bp < B || (Bp % 64) != 0 || Bp > GYM_MAX_BP || N < 2;
@@ -2463,6 +2488,7 @@ static bool bad_batch(const gym_batch* b) {
 
 int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, const gym_batch* b, void* s) {
     if (!m || !w || !x0 || bad_batch(b)) return GYM_EINVAL;
+    if ((b->flags & GYM_FLAG_REF_LANE) && (b->flags & GYM_FLAG_X_CKPT)) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const int T = b->N - 1;
     hipError_t e = hipMemsetAsync(b->u[0], 0, sizeof(double) * 2 * (size_t)T * b->Bp, st);
@@ -2475,7 +2501,8 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(b->stats, 0, sizeof(double) * 24, st);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_init, dim3(grid_for(b->Bp, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w), x0, b->u[0], b->x_ref, b->u_ref,
+    hipLaunchKernelGGL(((b->flags & GYM_FLAG_REF_LANE) ? k_init<true> : k_init<false>), dim3(grid_for(b->Bp, BLK)),
+                       dim3(BLK), 0, st, Dyn(*m), kw(*w), x0, b->u[0], b->x_ref, b->u_ref,
                        (double2*)b->x[0], b->cost, b->status, b->n_iter, b->res_buf, b->n_roll, b->gamma, b->smax,
                        b->dJ, b->B, b->Bp, b->N);
     return launch_status();
@@ -2491,18 +2518,18 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
     if (a->max_ls > 1 && n > 0) {
         {   // the lanes that reject trial 1 need sigma1: re-run their sweep of this iteration into its plane
             TimedLaunch tl(b->timing, 7, st);
-            hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m),
+            hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m),
                                kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
                                (const int32_t*)nullptr, -1, b->B, b->Bp, b->N);
         }
         {
             TimedLaunch tl(b->timing, 2, st);
             const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
-            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
+            hipLaunchKernelGGL(CAND_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
                                b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
                            b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
                            b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
     }
@@ -2531,14 +2558,14 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     const bool hist = a->record_history != 0;
     {
         TimedLaunch tl(b->timing, 0, st);
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
                            (double2*)b->K1, b->cs, a->gamma0, b->dJ, b->smax, b->status,
                            hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k, b->hist_len, 0};
     {
         TimedLaunch tl(b->timing, 1, st);
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, (const double2*)b->K1,
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_trial), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, (const double2*)b->K1,
                            (const double*)b->cs, b->x_ref, b->u_ref, b->cost, b->dJ, b->smax, b->gamma, b->status,
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
                            all, b->Bp, b->N);
@@ -2556,7 +2583,7 @@ int gym_newton_pipeline_split(const gym_batch* b, int64_t* Bh) {
 
 int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t p,
                      int32_t do_backward, void* s) {
-    if (bad_iter_args(m, w, a, b) || p < 0) return GYM_EINVAL;
+    if (bad_iter_args(m, w, a, b) || p < 0 || (b->flags & GYM_FLAG_REF_LANE)) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     int64_t Bh;
     gym_newton_pipeline_split(b, &Bh);
@@ -2596,7 +2623,8 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
 
 int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k0,
                    int32_t k1, void* s) {
-    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT)) return GYM_EINVAL;
+    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & (GYM_FLAG_X_CKPT | GYM_FLAG_REF_LANE)))
+        return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const bool hist = a->record_history != 0;
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k0, b->hist_len, 0};
@@ -2662,13 +2690,14 @@ int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* 
     hipStream_t st = (hipStream_t)s;
     const int T = b->N - 1;
     for (int parity = 0; parity < 2; ++parity) {   // sigma1 of each lane's last sweep, one launch per buffer
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_sigma), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
                            (const double2*)b->x[parity], b->u[parity], b->x_ref, b->u_ref, b->cs,
                            (const int32_t*)nullptr, (const int32_t*)nullptr, b->n_iter, parity, b->B, b->Bp, b->N);
         const int e = launch_status();
         if (e) return e;
     }
-    return launch_unpack_tiled(SrcSigma{kw(*w), b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter}, sig_out, b->B, b->Bp,
+    return launch_unpack_tiled(SrcSigma{kw(*w), b->cs, b->u[0], b->u[1], b->u_ref, b->n_iter,
+                                        (b->flags & GYM_FLAG_REF_LANE) ? 2 * (int64_t)(b->N - 1) : 0}, sig_out, b->B, b->Bp,
                                T, 2, st, b->lane_map);
 }
 
@@ -2691,7 +2720,7 @@ int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, c
 int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                            int32_t k, const double* gammas, int32_t G, double* cost_out, void* s) {
     if (!m || !w || !a || bad_batch(b) || k < 0 || !gammas || !cost_out || G < 1 ||
-        (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8)
+        (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8 || (b->flags & GYM_FLAG_REF_LANE))
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const TrialIO io = trial_io(b, k);

@@ -107,17 +107,22 @@ class AcrobotEngine:
                                              L, P * W, W, self.stream), "gym_unpack_lanes")
         return out
 
-    def refs(self, x_ref, u_ref):
+    def refs(self, x_ref, u_ref, per_lane: bool = False):
+        """(x_ref (N,4), u_ref (N-1,2)) on the device, u_ref trimmed / checked as newton_Algorithm does; with
+        ``per_lane`` also (B,N,4) / (B,N-1 or N,2) per-lane references (the batched solver's serial schedule)."""
         x_ref = self.t(x_ref)
         u_ref = self.t(u_ref)
-        if x_ref.ndim != 2 or x_ref.shape[1] != 4:
-            raise ValueError(f"x_ref must be (N,4), got {tuple(x_ref.shape)}")
-        if u_ref.shape[0] == x_ref.shape[0]:        # trajectory_generation.py:301-303
-            u_ref = u_ref[:-1].contiguous()
-        if u_ref.ndim != 2 or u_ref.shape[1] != 2 or u_ref.shape[0] != x_ref.shape[0] - 1:
-            raise ValueError(f"Incompatible dimensions: x_ref has {x_ref.shape[0]} states but u_ref has "
-                             f"{u_ref.shape[0]} controls (expected {x_ref.shape[0] - 1})")
-        return x_ref, u_ref
+        lane = per_lane and x_ref.ndim == 3
+        if (x_ref.ndim != (3 if lane else 2)) or x_ref.shape[-1] != 4:
+            raise ValueError(f"x_ref must be (N,4){' or (B,N,4)' if per_lane else ''}, got {tuple(x_ref.shape)}")
+        if u_ref.ndim != x_ref.ndim or u_ref.shape[-1] != 2 or (lane and u_ref.shape[0] != x_ref.shape[0]):
+            raise ValueError(f"u_ref {tuple(u_ref.shape)} does not match x_ref {tuple(x_ref.shape)}")
+        if u_ref.shape[-2] == x_ref.shape[-2]:      # trajectory_generation.py:301-303
+            u_ref = u_ref[..., :-1, :].contiguous()
+        if u_ref.shape[-2] != x_ref.shape[-2] - 1:
+            raise ValueError(f"Incompatible dimensions: x_ref has {x_ref.shape[-2]} states but u_ref has "
+                             f"{u_ref.shape[-2]} controls (expected {x_ref.shape[-2] - 1})")
+        return x_ref.contiguous(), u_ref.contiguous()
 
     # --------------------------------------------------------------------- point primitives
     def _points(self, x, u):

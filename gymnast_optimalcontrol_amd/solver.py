@@ -99,9 +99,22 @@ class BatchedNewtonSolver:
         # synchronise (all-reduce) at different points, and mixed choices would pair up the wrong collectives.
         sched_B = self.B_sched = int(schedule_lanes) if schedule_lanes is not None else int(B)
         self.eng = engine
-        self.x_ref, self.u_ref = engine.refs(x_ref, u_ref)
+        self.x_ref, self.u_ref = engine.refs(x_ref, u_ref, per_lane=True)
         self.B, self.Bp = int(B), padded(int(B))
-        self.N = int(self.x_ref.shape[0])
+        self.N = int(self.x_ref.shape[-2])
+        # per-lane references (x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE): the serial schedule only
+        self.ref_lane = self.x_ref.ndim == 3
+        if self.ref_lane:
+            if self.x_ref.shape[0] != self.B:
+                raise ValueError(f"per-lane references must hold {self.B} lanes, got {self.x_ref.shape[0]}")
+            if pipeline or persistent or checkpoint:
+                raise ValueError("per-lane references run the serial schedule only (no pipelined / persistent "
+                                 "schedule, no state checkpointing)")
+            pipeline, persistent = False, False
+            pad = self.Bp - self.B                     # padding lanes read valid rows (the last lane's)
+            self._xr_in, self._ur_in = self.x_ref, self.u_ref
+            self.xr_buf = torch.cat([self.x_ref, self.x_ref[-1:].expand(pad, -1, -1)]).contiguous()
+            self.ur_buf = torch.cat([self.u_ref, self.u_ref[-1:].expand(pad, -1, -1)]).contiguous()
         self.T = self.N - 1
         self.armijo = _lib.GymArmijo(float(tol), float(beta), float(c), float(gamma_0), int(max_ls),
                                      1 if hist_len > 0 else 0)
@@ -132,7 +145,7 @@ class BatchedNewtonSolver:
         b.B, b.Bp, b.N, b.hist_len = self.B, self.Bp, self.N, self.hist_len
         # tau1 is unactuated (dynamics.py:205); with u_ref[:,0] == 0 its controls stay exactly 0 and the
         # kernels skip their planes (GYM_FLAG_U0_ZERO) -- bit-identical results, 24 B/stage less traffic
-        ref_u0_zero = bool((self.u_ref[:, 0] == 0).all().item())
+        ref_u0_zero = bool((self.u_ref[..., 0] == 0).all().item())
         if u0_zero and not ref_u0_zero:
             raise ValueError("u0_zero=True requires u_ref[:, 0] == 0")
         self.u0_zero = ref_u0_zero if u0_zero is None else bool(u0_zero)
@@ -157,13 +170,16 @@ class BatchedNewtonSolver:
         # the cost and the stores off the lanes' dependency chains; same bits) unless split_waves=False
         self.split_waves = bool(split_waves)
         b.flags = ((_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0) |
-                   (0 if self.split_waves else _lib.FLAG_RUN_SINGLE))
+                   (0 if self.split_waves else _lib.FLAG_RUN_SINGLE) | (_lib.FLAG_REF_LANE if self.ref_lane else 0))
         b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
         b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
         for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
                      "retry_list", "counters", "cand_ok", "partials", "stats"):
             setattr(b, name, getattr(self, name).data_ptr())
-        b.x_ref, b.u_ref = self.x_ref.data_ptr(), self.u_ref.data_ptr()
+        if self.ref_lane:
+            b.x_ref, b.u_ref = self.xr_buf.data_ptr(), self.ur_buf.data_ptr()
+        else:
+            b.x_ref, b.u_ref = self.x_ref.data_ptr(), self.u_ref.data_ptr()
         b.hist_cost = _lib.ptr(self.hist_cost)
         b.hist_smax = _lib.ptr(self.hist_smax)
         self.batch = b
@@ -223,11 +239,14 @@ class BatchedNewtonSolver:
                 pass
 
     # --- the three stream-ordered phases (no host synchronisation inside) -----------------
-    def init(self, x0):
+    def init(self, x0, _ref_perm=None):
         self.lane_order = None
         x0 = self.eng.t(x0).reshape(-1, 4)
         if x0.shape[0] != self.B:
             raise ValueError(f"x0 must hold {self.B} lanes, got {x0.shape[0]}")
+        if self.ref_lane:   # the references in the lanes' internal order (solve()'s Morton order, or the caller's)
+            self.xr_buf[:self.B] = self._xr_in if _ref_perm is None else self._xr_in[_ref_perm]
+            self.ur_buf[:self.B] = self._ur_in if _ref_perm is None else self._ur_in[_ref_perm]
         self._x0 = x0
         _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
@@ -334,6 +353,8 @@ class BatchedNewtonSolver:
         from): J(gamma_g) of the trial rollout along iteration k's direction, (B, G); NaN for finished lanes.
         At the trial step sizes gamma_0 beta^i the values are the Armijo trials' costs bit for bit.  Runs
         iteration k's backward sweep, which that iteration recomputes identically, so the solve is unchanged."""
+        if self.ref_lane:
+            raise NotImplementedError("gamma sweeps take a shared reference (GYM_FLAG_REF_LANE: serial solves only)")
         g = self.eng.t(gammas).reshape(-1)
         G = int(g.numel())
         if G < 1:
@@ -379,7 +400,7 @@ class BatchedNewtonSolver:
             x0 = self.eng.t(x0).reshape(-1, 4)
             perm = morton_order(x0)
             x0 = x0[perm]
-        self.init(x0)
+        self.init(x0, _ref_perm=perm)
         self.lane_order = perm
         if perm is not None and self.capture_lanes is not None:
             inv = torch.empty_like(perm)

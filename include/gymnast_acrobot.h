@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 8
+#define GYM_ABI_VERSION 9
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -61,6 +61,11 @@ extern "C" {
                              * rebuilds them (gym_newton_finalize does so itself).                          */
 #define GYM_FLAG_RUN_SINGLE 4 /* gym_newton_run: the single-wavefront persistent kernel instead of the default
                                * two-wavefront one (helper wavefront per 64 lanes; same bits) */
+#define GYM_FLAG_REF_LANE 8  /* per-lane references: gym_batch.x_ref is (Bp, N, 4) and u_ref (Bp, T, 2), lane-major
+                              * (lane l follows rows l; padding lanes any valid rows).  The serial schedule only:
+                              * gym_newton_init / _iteration / _sigma / _finalize; gym_newton_phase, gym_newton_run and
+                              * gym_newton_gamma_sweep return GYM_EINVAL, as does X_CKPT with it.  Same per-lane
+                              * arithmetic as a shared reference (vector instead of scalar loads: the same bits). */
 #define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 
@@ -116,8 +121,8 @@ typedef struct gym_batch {
     double* u[2];       /* (T, 2, Bp) control planes tau1, tau2, double-buffered  */
     double* K1;         /* (T, Bp/64, 2, 64) double2 feedback gains, row 1, wave-blocked pairs */
     double* cs;         /* (T, 2, Bp) planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1 (re-runs only) */
-    const double* x_ref;/* (N,4) shared reference states                          */
-    const double* u_ref;/* (T,2) shared reference controls (already trimmed)      */
+    const double* x_ref;/* (N,4) shared reference states; (Bp,N,4) with GYM_FLAG_REF_LANE */
+    const double* u_ref;/* (T,2) shared reference controls (already trimmed); (Bp,T,2) per lane */
     double* cost;       /* (Bp) current J_k                                       */
     double* dJ;         /* (Bp) expected reduction sum g^T sigma                  */
     double* smax;       /* (Bp) max|sigma| of the last backward sweep             */

@@ -561,3 +561,42 @@ def test_lane_transposes_round_trip(eng, C, W):
     sel = (torch.arange(B) % 3 == 1).to(torch.int32)
     got = eng.unpack(sa, B, sb, sel.to(eng.device)).cpu()
     assert torch.equal(got, torch.where(sel.bool()[:, None, None], b, a))
+
+
+def test_per_lane_references(golden, task2_refs):
+    """Per-lane references (SURVEY 8(b)'s batched form: x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE, the serial
+    schedule): three references dealt round-robin over 150 lanes -- task 2's, task 2's with 0.8 u_ref, and task 1's
+    (a live tau1 channel) -- in Morton order.  Every lane is bit for bit the lane of the shared-reference solve of
+    its group; lane 0 (task 2's reference, x0 = 0) is the reference's task-2 trajectory."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr2, ur2, _ = task2_refs
+    g1 = golden("task1_solve")
+    refs = [(xr2, ur2), (xr2, 0.8 * ur2), (g1["x_ref"], g1["u_ref_full"][:-1])]
+    B = 150
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(31).uniform(-0.5, 0.5, (B, 2))
+    x0[0] = 0.0
+    x0[2] = g1["x0"]
+    which = np.arange(B) % 3
+    XR = np.stack([refs[w][0] for w in which]); UR = np.stack([refs[w][1] for w in which])
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, hist_len=450)
+    s = BatchedNewtonSolver(eng, XR, UR, B, **kw)
+    assert s.schedule == "serial" and s.ref_lane and not s.u0_zero
+    r = s.solve(x0, 450)
+    st = r.status.cpu().numpy()
+    assert (st[which == 0] == _lib.CONVERGED).all(), np.bincount(st[which == 0])
+    for w, (xr, ur) in enumerate(refs):
+        lanes = np.flatnonzero(which == w)
+        rg = BatchedNewtonSolver(eng, xr, ur, lanes.size, **kw).solve(x0[lanes], 450)
+        for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "hist_cost", "hist_smax"):
+            a = getattr(r, name).cpu().numpy()
+            a = a[:, lanes] if name.startswith("hist") else a[lanes]
+            assert np.array_equal(a, getattr(rg, name).cpu().numpy(), equal_nan=True), (w, name)
+    g = golden("task2_reference_output")
+    assert rel_l2(r.x[0].cpu().numpy(), g["x"]) < TOL_TRAJ and int(r.n_iter[0].item()) == 393
+    with pytest.raises(ValueError):
+        BatchedNewtonSolver(eng, XR, UR, B, pipeline=True, **kw)
+    with pytest.raises(ValueError):
+        BatchedNewtonSolver(eng, XR[:10], UR[:10], B, **kw)
