@@ -1373,7 +1373,7 @@ __device__ __forceinline__ pargs_t phase_args() {
     return (pargs_t)p;
 }
 
-template <bool U0Z, bool CK>
+template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
     GYM_CK_LDS(CK, U0Z);
     if ((int)blockIdx.x < args.nb_b) {
@@ -1382,11 +1382,13 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
         double d, s;
         {
             const pargs_t R = phase_args();
+            const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+            const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1));
             if (CK)
-                backward_solver_lane_ck<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, R->xr, R->ur, R->K1, R->cs,
+                backward_solver_lane_ck<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1, R->cs,
                                                          R->a.gamma0, ck_lds, l, R->Bp, R->N, d, s);
             else
-                backward_solver_lane<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, R->xr, R->ur, R->K1, R->cs,
+                backward_solver_lane<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1, R->cs,
                                                       R->a.gamma0, l, R->Bp, R->N, d, s);
         }
         const pargs_t Q = phase_args();
@@ -1400,7 +1402,9 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
         {   // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass)
             const pargs_t R = phase_args();
             const double2 xa = R->io.x[wix(0, 0, 2, l, R->Bp)], xb = R->io.x[wix(0, 1, 2, l, R->Bp)];
-            Jn = rollout_cform<true, U0Z, false, CK>(R->m, R->w, R->io.u, R->K1, R->cs, R->xr, R->ur, R->io.xn,
+            Jn = rollout_cform<true, U0Z, false, CK>(R->m, R->w, R->io.u, R->K1, R->cs,
+                                                     lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N),
+                                                     lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1)), R->io.xn,
                                                      R->io.un, R->a.gamma0, R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y,
                                                      xb.x, xb.y);
         }
@@ -2583,7 +2587,7 @@ int gym_newton_pipeline_split(const gym_batch* b, int64_t* Bh) {
 
 int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t p,
                      int32_t do_backward, void* s) {
-    if (bad_iter_args(m, w, a, b) || p < 0 || (b->flags & GYM_FLAG_REF_LANE)) return GYM_EINVAL;
+    if (bad_iter_args(m, w, a, b) || p < 0) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     int64_t Bh;
     gym_newton_pipeline_split(b, &Bh);
@@ -2613,7 +2617,7 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
         pa.retry_list = b->retry_list; pa.counter = b->counters + ht;
         pa.hist_cost = hist ? b->hist_cost : nullptr; pa.hist_smax = hist ? b->hist_smax : nullptr;
         pa.rb = rb; pa.rt = rt; pa.Bp = b->Bp; pa.N = b->N; pa.kb = kb; pa.nb_b = nb_b; pa.pad = 0;
-        hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, pa);
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, pa);
     }
     if (p >= 1)  // the trial half's retries and statistics; H1 closes the iteration: total = H0 + H1
         launch_post_trial(m, w, a, b, c, io, rt, b->counters + ht, b->stats + 8 + 8 * ht,

@@ -565,9 +565,10 @@ def test_lane_transposes_round_trip(eng, C, W):
 
 def test_per_lane_references(golden, task2_refs):
     """Per-lane references (SURVEY 8(b)'s batched form: x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE, the serial
-    schedule): three references dealt round-robin over 150 lanes -- task 2's, task 2's with 0.8 u_ref, and task 1's
+    and pipelined schedules): three references dealt round-robin over 150 lanes -- task 2's, task 2's with 0.8 u_ref, and task 1's
     (a live tau1 channel) -- in Morton order.  Every lane is bit for bit the lane of the shared-reference solve of
-    its group; lane 0 (task 2's reference, x0 = 0) is the reference's task-2 trajectory."""
+    its group, and the pipelined solve bit for bit the serial one; lane 0 (task 2's reference, x0 = 0) is the
+    reference's task-2 trajectory."""
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
@@ -596,7 +597,10 @@ def test_per_lane_references(golden, task2_refs):
             assert np.array_equal(a, getattr(rg, name).cpu().numpy(), equal_nan=True), (w, name)
     g = golden("task2_reference_output")
     assert rel_l2(r.x[0].cpu().numpy(), g["x"]) < TOL_TRAJ and int(r.n_iter[0].item()) == 393
+    rp = BatchedNewtonSolver(eng, XR, UR, B, pipeline=True, **kw).solve(x0, 450)   # the pipelined schedule too
+    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "hist_cost", "hist_smax"):
+        assert np.array_equal(getattr(r, name).cpu().numpy(), getattr(rp, name).cpu().numpy(), equal_nan=True), name
     with pytest.raises(ValueError):
-        BatchedNewtonSolver(eng, XR, UR, B, pipeline=True, **kw)
+        BatchedNewtonSolver(eng, XR, UR, B, persistent=True, **kw)
     with pytest.raises(ValueError):
         BatchedNewtonSolver(eng, XR[:10], UR[:10], B, **kw)
