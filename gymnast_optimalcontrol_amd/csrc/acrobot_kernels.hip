@@ -1540,6 +1540,16 @@ __device__ __forceinline__ rargs_t run_args() {
     return (rargs_t)p;
 }
 
+// the lane's reference rows in the persistent kernels (per-lane references: GYM_FLAG_REF_LANE)
+template <bool RL>
+__device__ __forceinline__ const double* run_xr(rargs_t R, int64_t l) {
+    return lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+}
+template <bool RL>
+__device__ __forceinline__ const double* run_ur(rargs_t R, int64_t l) {
+    return lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1));
+}
+
 __device__ __forceinline__ void lane_fence() {   // this lane's stores visible to its own later loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
 }
@@ -1552,7 +1562,7 @@ __device__ unsigned long long g_run2_trace[8192][2][6];
 #else
 #define R2T_NOW() 0ull
 #endif
-template <bool U0Z>
+template <bool U0Z, bool RL>
 __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
     constexpr bool BAND = GYM_RUN_BAND == 1;
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -1577,10 +1587,12 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
             const rargs_t R = run_args();
             double d, s;
             if (GYM_RUN_ILP)
-                backward_solver_lane_ilp<U0Z, OUT_SOLVER>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1,
+                backward_solver_lane_ilp<U0Z, OUT_SOLVER>(R->m, R->w, R->x[cb], R->u[cb], run_xr<RL>(R, l),
+                                                          run_ur<RL>(R, l), R->K1,
                                                           R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
             else
-                backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], R->xr, R->ur, R->K1,
+                backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], run_xr<RL>(R, l),
+                                                            run_ur<RL>(R, l), R->K1,
                                                             R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
             const rargs_t Q = run_args();
             Q->dJ[l] = d;
@@ -1594,7 +1606,8 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
         {
             const rargs_t R = run_args();
             const double2 xa = R->x[cb][wix(0, 0, 2, l, R->Bp)], xb = R->x[cb][wix(0, 1, 2, l, R->Bp)];
-            Jn = rollout_cform<true, U0Z, false, false, kNT, BAND>(R->m, R->w, R->u[cb], R->K1, R->cs, R->xr, R->ur,
+            Jn = rollout_cform<true, U0Z, false, false, kNT, BAND>(R->m, R->w, R->u[cb], R->K1, R->cs,
+                                                                   run_xr<RL>(R, l), run_ur<RL>(R, l),
                                                                    R->x[cb ^ 1], R->u[cb ^ 1], R->a.gamma0,
                                                                    R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y, xb.x, xb.y);
         }
@@ -1608,7 +1621,8 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
             {
                 const rargs_t P = run_args();
                 double d2, s2;
-                backward_solver_lane<U0Z, OUT_SIGMA, BAND>(P->m, P->w, P->x[cb], P->u[cb], P->xr, P->ur, P->K1,
+                backward_solver_lane<U0Z, OUT_SIGMA, BAND>(P->m, P->w, P->x[cb], P->u[cb], run_xr<RL>(P, l),
+                                                           run_ur<RL>(P, l), P->K1,
                                                            P->cs, 0.0, l, P->Bp, P->N, d2, s2);
             }
             lane_fence();
@@ -1616,8 +1630,8 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
                 const rargs_t P = run_args();
                 g *= P->a.beta;   // gamma_i *= beta, sequentially (:365)
                 const double2 xa = P->x[cb][wix(0, 0, 2, l, P->Bp)], xb = P->x[cb][wix(0, 1, 2, l, P->Bp)];
-                Jn = rollout_cform<true, U0Z, true, false, kNT, BAND>(P->m, P->w, P->u[cb], P->K1, P->cs, P->xr,
-                                                                      P->ur, P->x[cb ^ 1], P->u[cb ^ 1], g,
+                Jn = rollout_cform<true, U0Z, true, false, kNT, BAND>(P->m, P->w, P->u[cb], P->K1, P->cs,
+                                                                      run_xr<RL>(P, l), run_ur<RL>(P, l), P->x[cb ^ 1], P->u[cb ^ 1], g,
                                                                       P->a.gamma0, l, P->Bp, P->N, xa.x, xa.y, xb.x,
                                                                       xb.y);
                 ++nr;
@@ -1705,6 +1719,15 @@ __device__ __forceinline__ Row<NV> const_row(const double* base, int t) {
     for (int i = 0; i < NV; ++i) r.v[i] = p[i];
     return r;
 }
+// ... or, for per-lane references, the lane's own row (vector loads)
+template <int NV, bool RL>
+__device__ __forceinline__ Row<NV> ref_row(const double* base, int t) {
+    if (!RL) return const_row<NV>(base, t);
+    Row<NV> r;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) r.v[i] = base[(int64_t)NV * t + i];
+    return r;
+}
 __device__ __forceinline__ void in_vgpr2(double2& v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
 __device__ __forceinline__ int run2_chunks(int T) {
     constexpr int per = R2PD / R2C;
@@ -1725,7 +1748,7 @@ __device__ __forceinline__ void lds_barrier(unsigned long long& wait) {
 
 // helper wavefront HID of NH, sweep: the stages i = HID, HID + NH, ... of the reverse pass (t = T-1-i) into slot
 // (chunk & 1) * R2C + (i % R2C)
-template <bool U0Z, int HID, int NH>
+template <bool U0Z, int HID, int NH, bool RL>
 __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t l, int cb, const double* __restrict__ xr,
                                                   const double* __restrict__ ur, unsigned long long& bw) {
     const rargs_t R = run_args();
@@ -1734,7 +1757,8 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
     const uint32_t row = (uint32_t)R->Bp * 16u, plane = (uint32_t)R->Bp * 8u;
     const char* Xb = reinterpret_cast<const char*>(R->x[cb]);
     const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
-    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them)
+    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them); per-lane
+    // references (RL): the lane's own rows
     const gym::PolyRegs pk = gym::poly_vgprs();
     auto fetch = [&](SweepStage& q, int t) {
         const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)t * row);
@@ -1746,8 +1770,8 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
     auto produce = [&](const SweepStage& q, int t, int slot) {
         const KArgs ka = kernarg_consts();
         const gym::Jac J = gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
-        const Row<4> xrt = const_row<4>(xr, t);
-        const Row<2> urt = const_row<2>(ur, t);
+        const Row<4> xrt = ref_row<4, RL>(xr, t);
+        const Row<2> urt = ref_row<2, RL>(ur, t);
         const Lin L = stage_lin(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
         double2(*s)[BLK] = ring[slot];
         s[0][lane] = q.xa;                          s[1][lane] = q.xb;
@@ -1786,7 +1810,7 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
 }
 
 // main wavefront, sweep: the Riccati recursion from the ring; K row 1 / cg stored for active lanes
-template <bool U0Z>
+template <bool U0Z, bool RL>
 __device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l, int cb, bool act, double& dJ_out,
                                                 double& smax_out, unsigned long long& bw) {
     const rargs_t R = run_args();
@@ -1798,7 +1822,7 @@ __device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l
     const char* Cb = reinterpret_cast<const char*>(R->cs);
     const double g0 = R->a.gamma0;
     const double2* x = R->x[cb];
-    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], R->xr + 4 * T);
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], run_xr<RL>(R, l) + 4 * T);
     const int nch = run2_chunks(T);
     lds_barrier(bw);                       // the helper's chunk 0
     for (int c = 0; c < nch; ++c) {
@@ -1935,7 +1959,7 @@ __device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_
 }
 
 // helper wavefront, first Armijo trial: u0, the running cost and the candidate's stores; returns J
-template <bool U0Z>
+template <bool U0Z, bool RL>
 __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64_t l, int cb, bool act,
                                                   const double* __restrict__ xr, const double* __restrict__ ur,
                                                   unsigned long long& bw) {
@@ -1947,7 +1971,8 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
     const char* Xb = reinterpret_cast<const char*>(R->x[cb ^ 1]);
     const char* Ob = reinterpret_cast<const char*>(R->u[cb ^ 1]);
-    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them)
+    // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them); per-lane
+    // references (RL): the lane's own rows
     const double gamma = R->a.gamma0;
     const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
     double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
@@ -1966,8 +1991,8 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
             if (t < T) {
                 const double2(*s)[BLK] = ring[(c & 1) * R2C + j];
                 const double2 na = s[0][lane], nb = s[1][lane], vv = s[2][lane];
-                const Row<2> urt = const_row<2>(ur, t);
-                const Row<4> xrt = const_row<4>(xr, t);
+                const Row<2> urt = ref_row<2, RL>(ur, t);
+                const Row<4> xrt = ref_row<4, RL>(xr, t);
                 const KArgs ka = kernarg_consts();
                 const double u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
                 const double v0 = trial_u0(u0, urt.v[0], gamma, ka.w.G00, ka.w.iG00);
@@ -1987,7 +2012,7 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
         }
         lds_barrier(bw);
     }
-    const Row<4> xrT = const_row<4>(xr, T);
+    const Row<4> xrT = ref_row<4, RL>(xr, T);
     return J + xcost(R->w.QT, n0, n1, n2, n3, xrT.v);
 }
 
@@ -2010,7 +2035,7 @@ __device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
     for (int c = 0; c <= nch; ++c) lds_barrier(bw);
 }
 
-template <bool U0Z>
+template <bool U0Z, bool RL>
 __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
     __shared__ double2 ring[R2S][R2W][BLK];
     __shared__ double shJ[BLK];
@@ -2029,14 +2054,16 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
         unsigned long long tt = R2T_NOW();
         ++acc[3];
         if (wave == 1) {
-            run2_sweep_helper<U0Z, 0, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
+            run2_sweep_helper<U0Z, 0, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l), run_ur<RL>(run_args(), l),
+                                               acc[4]);
         } else if (wave == 2 && R2H == 2) {
-            run2_sweep_helper<U0Z, R2H - 1, R2H>(ring, lane, l, cb, run_args()->xr, run_args()->ur, acc[4]);
+            run2_sweep_helper<U0Z, R2H - 1, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l),
+                                                     run_ur<RL>(run_args(), l), acc[4]);
         } else if (wave > R2H) {
             run2_idle(run_args()->N - 1, acc[4]);
         } else {
             double d, s;
-            run2_sweep_main<U0Z>(ring, lane, l, cb, act, d, s, acc[4]);
+            run2_sweep_main<U0Z, RL>(ring, lane, l, cb, act, d, s, acc[4]);
             const rargs_t Q = run_args();
             if (act) {
                 Q->dJ[l] = d;
@@ -2049,7 +2076,8 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
         acc[0] += R2T_NOW() - tt;
         tt = R2T_NOW();
         if (wave == 1) {
-            shJ[lane] = run2_trial_helper<U0Z>(ring, lane, l, cb, act, run_args()->xr, run_args()->ur, acc[5]);
+            shJ[lane] = run2_trial_helper<U0Z, RL>(ring, lane, l, cb, act, run_xr<RL>(run_args(), l),
+                                                   run_ur<RL>(run_args(), l), acc[5]);
         } else if (wave == 2 && R2H == 2) {
             run2_idle(run_args()->N - 1, acc[5]);
         } else if (R2P) {                                  // wave 0 and wave R2H + 1: lane pairs
@@ -2072,7 +2100,8 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
                 {
                     const rargs_t P = run_args();
                     double d2, s2;
-                    backward_solver_lane<U0Z, OUT_SIGMA, false>(P->m, P->w, P->x[cb], P->u[cb], P->xr, P->ur, P->K1,
+                    backward_solver_lane<U0Z, OUT_SIGMA, false>(P->m, P->w, P->x[cb], P->u[cb], run_xr<RL>(P, l),
+                                                                run_ur<RL>(P, l), P->K1,
                                                                 P->cs, 0.0, l, P->Bp, P->N, d2, s2);
                 }
                 lane_fence();
@@ -2080,8 +2109,9 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
                     const rargs_t P = run_args();
                     g *= P->a.beta;                        // gamma_i *= beta, sequentially (:365)
                     const double2 xa = P->x[cb][wix(0, 0, 2, l, P->Bp)], xb = P->x[cb][wix(0, 1, 2, l, P->Bp)];
-                    Jn = rollout_cform<true, U0Z, true, false, kNT, false>(P->m, P->w, P->u[cb], P->K1, P->cs, P->xr,
-                                                                          P->ur, P->x[cb ^ 1], P->u[cb ^ 1], g,
+                    Jn = rollout_cform<true, U0Z, true, false, kNT, false>(P->m, P->w, P->u[cb], P->K1, P->cs,
+                                                                          run_xr<RL>(P, l), run_ur<RL>(P, l),
+                                                                          P->x[cb ^ 1], P->u[cb ^ 1], g,
                                                                           P->a.gamma0, l, P->Bp, P->N, xa.x, xa.y,
                                                                           xb.x, xb.y);
                     ++nr;
@@ -2322,6 +2352,7 @@ struct TimedLaunch {  // records a start/stop event pair around one launch if th
     (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false, true>              \
                                                                           : kern<false, false, true>)           \
                                       : SOLVER_SEL(b, kern))
+#define RUN_SEL(b, kern) CAND_SEL(b, kern)   // the persistent kernels: <U0Z, RL>
 #define CAND_SEL(b, kern)                                                                                        \
     (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, true> : kern<false, true>) \
                                       : (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false> : kern<false, false>))
@@ -2627,7 +2658,7 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
 
 int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k0,
                    int32_t k1, void* s) {
-    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & (GYM_FLAG_X_CKPT | GYM_FLAG_REF_LANE)))
+    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT))
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const bool hist = a->record_history != 0;
@@ -2645,9 +2676,9 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
         ra.hist_cost = hist ? b->hist_cost : nullptr; ra.hist_smax = hist ? b->hist_smax : nullptr;
         ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.pad = 0;
         if (b->flags & GYM_FLAG_RUN_SINGLE)
-            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
+            hipLaunchKernelGGL(RUN_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
         else   // two wavefronts per 64 lanes; every lane of the padded batch takes part (padding: GYM_PAD)
-            hipLaunchKernelGGL(U0Z_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3(R2WAVES * BLK), 0, st, ra);
+            hipLaunchKernelGGL(RUN_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3(R2WAVES * BLK), 0, st, ra);
     }
     // the statistics after iteration k1 - 1 ("lanes that ran" = the lanes that executed it; [4] = 0: this
     // schedule keeps no retry list)

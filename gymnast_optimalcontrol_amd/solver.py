@@ -102,16 +102,14 @@ class BatchedNewtonSolver:
         self.x_ref, self.u_ref = engine.refs(x_ref, u_ref, per_lane=True)
         self.B, self.Bp = int(B), padded(int(B))
         self.N = int(self.x_ref.shape[-2])
-        # per-lane references (x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE): the serial and pipelined
-        # schedules (the automatic choice among those two), no state checkpointing
+        # per-lane references (x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE): every schedule, no state
+        # checkpointing
         self.ref_lane = self.x_ref.ndim == 3
         if self.ref_lane:
             if self.x_ref.shape[0] != self.B:
                 raise ValueError(f"per-lane references must hold {self.B} lanes, got {self.x_ref.shape[0]}")
-            if persistent or checkpoint:
-                raise ValueError("per-lane references run the serial or pipelined schedule (no persistent schedule, "
-                                 "no state checkpointing)")
-            persistent = False
+            if checkpoint:
+                raise ValueError("per-lane references do not combine with state checkpointing")
             pad = self.Bp - self.B                     # padding lanes read valid rows (the last lane's)
             self._xr_in, self._ur_in = self.x_ref, self.u_ref
             self.xr_buf = torch.cat([self.x_ref, self.x_ref[-1:].expand(pad, -1, -1)]).contiguous()

@@ -564,11 +564,12 @@ def test_lane_transposes_round_trip(eng, C, W):
 
 
 def test_per_lane_references(golden, task2_refs):
-    """Per-lane references (SURVEY 8(b)'s batched form: x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE, the serial
-    and pipelined schedules): three references dealt round-robin over 150 lanes -- task 2's, task 2's with 0.8 u_ref, and task 1's
+    """Per-lane references (SURVEY 8(b)'s batched form: x_ref (B,N,4), u_ref (B,T,2); GYM_FLAG_REF_LANE, every
+    schedule): three references dealt round-robin over 150 lanes -- task 2's, task 2's with 0.8 u_ref, and task 1's
     (a live tau1 channel) -- in Morton order.  Every lane is bit for bit the lane of the shared-reference solve of
-    its group, and the pipelined solve bit for bit the serial one; lane 0 (task 2's reference, x0 = 0) is the
-    reference's task-2 trajectory."""
+    its group, and the serial, pipelined and single-wavefront persistent solves bit for bit the default
+    (persistent, four wavefronts per 64 lanes) one; lane 0 (task 2's reference, x0 = 0) is the reference's task-2
+    trajectory."""
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
@@ -584,7 +585,7 @@ def test_per_lane_references(golden, task2_refs):
     eng = AcrobotEngine()
     kw = dict(tol=1e-4, gamma_0=0.1, hist_len=450)
     s = BatchedNewtonSolver(eng, XR, UR, B, **kw)
-    assert s.schedule == "serial" and s.ref_lane and not s.u0_zero
+    assert s.schedule == "persistent" and s.ref_lane and not s.u0_zero
     r = s.solve(x0, 450)
     st = r.status.cpu().numpy()
     assert (st[which == 0] == _lib.CONVERGED).all(), np.bincount(st[which == 0])
@@ -597,10 +598,12 @@ def test_per_lane_references(golden, task2_refs):
             assert np.array_equal(a, getattr(rg, name).cpu().numpy(), equal_nan=True), (w, name)
     g = golden("task2_reference_output")
     assert rel_l2(r.x[0].cpu().numpy(), g["x"]) < TOL_TRAJ and int(r.n_iter[0].item()) == 393
-    rp = BatchedNewtonSolver(eng, XR, UR, B, pipeline=True, **kw).solve(x0, 450)   # the pipelined schedule too
-    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "hist_cost", "hist_smax"):
-        assert np.array_equal(getattr(r, name).cpu().numpy(), getattr(rp, name).cpu().numpy(), equal_nan=True), name
+    for sched in (dict(pipeline=False, persistent=False), dict(pipeline=True), dict(split_waves=False)):
+        rp = BatchedNewtonSolver(eng, XR, UR, B, **sched, **kw).solve(x0, 450)
+        for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "hist_cost", "hist_smax"):
+            assert np.array_equal(getattr(r, name).cpu().numpy(), getattr(rp, name).cpu().numpy(),
+                                  equal_nan=True), (sched, name)
     with pytest.raises(ValueError):
-        BatchedNewtonSolver(eng, XR, UR, B, persistent=True, **kw)
+        BatchedNewtonSolver(eng, XR, UR, B, checkpoint=True, **kw)
     with pytest.raises(ValueError):
         BatchedNewtonSolver(eng, XR[:10], UR[:10], B, **kw)
