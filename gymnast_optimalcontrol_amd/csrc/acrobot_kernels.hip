@@ -2181,7 +2181,7 @@ __global__ __launch_bounds__(BLK) void k_gamma_sweep(Dyn m, KW w, const double2*
 
 // solver form: the Armijo trial's own rollout (offset form) on a batch's iteration-k streams; at the
 // trial's step sizes the costs are bit-identical to the trial's.  Non-active lanes get NaN.
-template <bool U0Z>
+template <bool U0Z, bool RL>
 __global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const double2* __restrict__ x,
                                                         const double* __restrict__ u, const double2* __restrict__ K1,
                                                         const double* __restrict__ cs, double g0,
@@ -2198,9 +2198,9 @@ __global__ __launch_bounds__(BLK) void k_nt_gamma_sweep(Dyn m, KW w, const doubl
         return;
     }
     const double2 a = x[wix(0, 0, 2, l, Bp)], b = x[wix(0, 1, 2, l, Bp)];
-    cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, true, false, 0>(m, w, u, K1, cs, xr, ur, nullptr,
-                                                                              nullptr, gammas[g], g0, l, Bp, N, a.x,
-                                                                              a.y, b.x, b.y);
+    cost_out[(int64_t)g * Bp + l] = rollout_cform<false, U0Z, true, false, 0>(
+        m, w, u, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N), lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), nullptr,
+        nullptr, gammas[g], g0, l, Bp, N, a.x, a.y, b.x, b.y);
 }
 
 // Deterministic two-stage statistics reduction (fixed lane->thread map, fixed trees).
@@ -2755,17 +2755,17 @@ int gym_gamma_sweep(const gym_model* m, const gym_weights* w, const double* x, c
 int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                            int32_t k, const double* gammas, int32_t G, double* cost_out, void* s) {
     if (!m || !w || !a || bad_batch(b) || k < 0 || !gammas || !cost_out || G < 1 ||
-        (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8 || (b->flags & GYM_FLAG_REF_LANE))
+        (b->Bp / BLK) * (int64_t)G > ((int64_t)1 << 31) - 8)
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const TrialIO io = trial_io(b, k);
     // iteration k's backward sweep (K1, cg, dJ, smax: the values iteration k itself computes) plus sigma1
-    hipLaunchKernelGGL(SOLVER_SEL(b, k_nt_backward_all), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+    hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_backward_all), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
                        io.x, io.u, b->x_ref, b->u_ref, (double2*)b->K1, b->cs, a->gamma0, b->dJ, b->smax, b->status,
                        (double*)nullptr, Range{0, b->B}, b->Bp, b->N, (int)k, 0);
     int e = launch_status();
     if (e) return e;
-    hipLaunchKernelGGL(U0Z_SEL(b, k_nt_gamma_sweep), dim3(sweep_grid(b->Bp, G)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
+    hipLaunchKernelGGL(CAND_SEL(b, k_nt_gamma_sweep), dim3(sweep_grid(b->Bp, G)), dim3(BLK), 0, st, Dyn(*m), kw(*w),
                        io.x, io.u, (const double2*)b->K1, (const double*)b->cs, a->gamma0, gammas, (int)G, b->x_ref, b->u_ref,
                        b->status, cost_out, b->B, b->Bp, b->N);
     return launch_status();

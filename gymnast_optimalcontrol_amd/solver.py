@@ -352,8 +352,6 @@ class BatchedNewtonSolver:
         from): J(gamma_g) of the trial rollout along iteration k's direction, (B, G); NaN for finished lanes.
         At the trial step sizes gamma_0 beta^i the values are the Armijo trials' costs bit for bit.  Runs
         iteration k's backward sweep, which that iteration recomputes identically, so the solve is unchanged."""
-        if self.ref_lane:
-            raise NotImplementedError("gamma sweeps take a shared reference (GYM_FLAG_REF_LANE: serial solves only)")
         g = self.eng.t(gammas).reshape(-1)
         G = int(g.numel())
         if G < 1:

@@ -63,8 +63,8 @@ extern "C" {
                                * two-wavefront one (helper wavefront per 64 lanes; same bits) */
 #define GYM_FLAG_REF_LANE 8  /* per-lane references: gym_batch.x_ref is (Bp, N, 4) and u_ref (Bp, T, 2), lane-major
                               * (lane l follows rows l; padding lanes any valid rows).  Every schedule
-                              * (gym_newton_init / _iteration / _phase / _run / _sigma / _finalize);
-                              * gym_newton_gamma_sweep returns GYM_EINVAL, as does X_CKPT with it.  Same per-lane
+                              * (gym_newton_init / _iteration / _phase / _run / _sigma / _finalize) and
+                              * gym_newton_gamma_sweep; X_CKPT with it: GYM_EINVAL.  Same per-lane
                               * arithmetic as a shared reference (vector instead of scalar loads: the same bits). */
 #define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */

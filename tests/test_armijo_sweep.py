@@ -71,16 +71,20 @@ def test_newton_algorithm_armijo_reports_match_reference(golden, monkeypatch):
         np.testing.assert_allclose(np.asarray(a[2]), g["k0_K"], rtol=1e-8, atol=1e-12)
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_solver_gamma_sweep_equals_trial_costs_and_leaves_solve_unchanged(task2_refs, pipeline):
+@pytest.mark.parametrize("pipeline,per_lane", [(False, False), (True, False), (False, True)])
+def test_solver_gamma_sweep_equals_trial_costs_and_leaves_solve_unchanged(task2_refs, pipeline, per_lane):
     """BatchedNewtonSolver.gamma_sweep at the trial step sizes gamma_0 beta^i gives the Armijo trials' costs
     bit for bit (accepted step: the lane's new J; rejected ones fail the strict test), for every lane; and a
-    solve with sweeps between its iterations is bitwise the solve without them."""
+    solve with sweeps between its iterations is bitwise the solve without them.  per_lane: task 2's reference and
+    the same with 0.8 u_ref on alternate lanes (GYM_FLAG_REF_LANE)."""
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
     from gymnast_optimalcontrol_amd import _lib
     xr, ur, _ = task2_refs
     B = 300
+    if per_lane:
+        alt = (np.arange(B) % 2 == 1)[:, None, None]
+        xr, ur = np.broadcast_to(xr, (B,) + xr.shape).copy(), np.where(alt, 0.8 * ur, ur)
     x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(8).uniform(-1.5, 1.5, (B, 2))
     eng = AcrobotEngine()
     # gamma_0 = 1 (the reference's default, :298): full steps backtrack from the first iterations and many lanes
