@@ -454,6 +454,49 @@ def test_persistent_schedule_matches_serial(task2_refs, max_iters, chunk, u0z, s
         assert (st == _lib.MAX_ITERS).any()
 
 
+@pytest.mark.parametrize("N", [2, 3, 4, 6, 37, 203])
+def test_every_schedule_on_short_and_ragged_horizons(task2_refs, N):
+    """Horizons from one stage (N = 2) up, odd ones, and ones shorter than the persistent kernel's chunk (2 stages)
+    and prefetch distance (4 stages) or the ILP sweep's unroll (6): the serial, pipelined and persistent (four- and
+    single-wavefront) solves are bitwise equal, lane by lane (incl. a NaN lane); the serial one has the C oracle's
+    decisions and its trajectories within 1e-8; a one-lane batch is bitwise its lane of the 130-lane batch."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from oracle import c_oracle
+    xr, ur, _ = task2_refs
+    xr, ur = xr[:N], ur[:N - 1]
+    B, max_iters = 130, 300
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(60 + N).uniform(-1.5, 1.5, (B, 2))
+    x0[3] = np.nan
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, hist_len=16)
+    names = ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax")
+    rs = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, persistent=False, **kw).solve(x0, max_iters)
+    assert rs.schedule == "serial"
+    for sched in (dict(pipeline=True), dict(persistent=True), dict(persistent=True, split_waves=False)):
+        r = BatchedNewtonSolver(eng, xr, ur, B, **sched, **kw).solve(x0, max_iters)
+        for name in names:
+            assert np.array_equal(getattr(rs, name).cpu().numpy(), getattr(r, name).cpu().numpy(),
+                                  equal_nan=True), (sched, name)
+    for sched in (dict(pipeline=False, persistent=False), dict(pipeline=True), dict(persistent=True)):
+        r1 = BatchedNewtonSolver(eng, xr, ur, 1, **sched, **kw).solve(x0[5:6], max_iters)
+        for name in names:
+            a = getattr(rs, name).cpu().numpy()
+            a = a[:, 5:6] if name.startswith("hist") else a[5:6]
+            assert np.array_equal(a, getattr(r1, name).cpu().numpy(), equal_nan=True), (sched, name)
+    st = rs.status.cpu().numpy()
+    assert st[3] == _lib.LS_FAILED
+    ok = np.arange(B) != 3
+    o = c_oracle.newton_solve(x0[ok], xr, ur, max_iters=max_iters, tol=1e-4, gamma_0=0.1)
+    np.testing.assert_array_equal(rs.n_iter.cpu().numpy()[ok], o["n_iter"])
+    np.testing.assert_array_equal(st[ok], o["status"])
+    np.testing.assert_array_equal(rs.n_rollouts.cpu().numpy()[ok], o["n_rollouts"])
+    for name in ("x", "u"):
+        a, e = getattr(rs, name).cpu().numpy()[ok].reshape(B - 1, -1), o[name].reshape(B - 1, -1)
+        assert (np.linalg.norm(a - e, axis=1) / np.linalg.norm(e, axis=1)).max() < TOL_TRAJ, name
+
+
 @pytest.mark.parametrize("pipeline", [False, True])
 def test_lane_reordering_is_invisible(task2_refs, pipeline):
     """solve() runs the lanes in the Morton order of their initial states and writes the results back in the
