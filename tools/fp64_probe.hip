@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 
 constexpr int ITERS = 4096;
 
@@ -21,6 +22,30 @@ __global__ void k_fma_chains(const double* in, double* out, long long* cyc) {
     for (int i = 0; i < ITERS; ++i) {
 #pragma unroll
         for (int c = 0; c < CHAINS; ++c) x[c] = __builtin_fma(x[c], a, b);
+    }
+    double s = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) s += x[c];
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    if (threadIdx.x % 64 == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) / 64] = t1 - t0;
+}
+
+// the same chains with only the wave's first ACTIVE lanes executing the loop (exec mask): does a partly masked
+// fp64 instruction issue faster than a full one (fewer 16-lane passes)?
+template <int CHAINS, int ACTIVE>
+__global__ void k_fma_masked(const double* in, double* out, long long* cyc) {
+    double x[CHAINS];
+    const double a = in[0], b = in[1];
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) x[c] = in[2 + c] + threadIdx.x;
+    __syncthreads();
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) < ACTIVE) {
+        for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+            for (int c = 0; c < CHAINS; ++c) x[c] = __builtin_fma(x[c], a, b);
+        }
     }
     double s = 0;
 #pragma unroll
@@ -96,6 +121,18 @@ int main() {
     // 1 block of 64: one wave alone on a SIMD; 1024 blocks of 256: 4 waves per CU = one per SIMD on every CU;
     // 1024 blocks of 512: two waves per SIMD
     // 1 block of 128: are the two wavefronts of a workgroup on different SIMDs? (4.4 cyc/instr if so, ~6.5 if not)
+    if (getenv("PROBE_MASK")) {
+        run("masked: 64 lanes, chains=4", k_fma_masked<4, 64>, 1, 64, 4, din, dout, dcyc);
+        run("masked: 32 lanes, chains=4", k_fma_masked<4, 32>, 1, 64, 4, din, dout, dcyc);
+        run("masked: 16 lanes, chains=4", k_fma_masked<4, 16>, 1, 64, 4, din, dout, dcyc);
+        run("masked: 8 lanes, chains=4", k_fma_masked<4, 8>, 1, 64, 4, din, dout, dcyc);
+        run("masked: 64 lanes, chains=1", k_fma_masked<1, 64>, 1, 64, 1, din, dout, dcyc);
+        run("masked: 32 lanes, chains=1", k_fma_masked<1, 32>, 1, 64, 1, din, dout, dcyc);
+        run("masked: 16 lanes, chains=1", k_fma_masked<1, 16>, 1, 64, 1, din, dout, dcyc);
+        run("masked: 32 lanes, chains=4, 1024x256", k_fma_masked<4, 32>, 1024, 256, 4, din, dout, dcyc);
+        run("masked: 64 lanes, chains=4, 1024x256", k_fma_masked<4, 64>, 1024, 256, 4, din, dout, dcyc);
+        return 0;
+    }
     run("fma chains=4, 1 block x 128", k_fma_chains<4>, 1, 128, 4, din, dout, dcyc);
     run("fma chains=4, 256 blocks x 128", k_fma_chains<4>, 256, 128, 4, din, dout, dcyc);
     for (int thr : {64, 256, 512}) {
