@@ -109,7 +109,7 @@ class AcrobotEngine:
 
     def refs(self, x_ref, u_ref, per_lane: bool = False):
         """(x_ref (N,4), u_ref (N-1,2)) on the device, u_ref trimmed / checked as newton_Algorithm does; with
-        ``per_lane`` also (B,N,4) / (B,N-1 or N,2) per-lane references (the batched solver's serial / pipelined schedules)."""
+        ``per_lane`` also (B,N,4) / (B,N-1 or N,2) per-lane references (the batched solver, every schedule)."""
         x_ref = self.t(x_ref)
         u_ref = self.t(u_ref)
         lane = per_lane and x_ref.ndim == 3

@@ -398,7 +398,7 @@ def newton_Algorithm_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.
                            max_ls=MAX_LINE_SEARCH_ITERS, hist_len=0, reduce_stats=None,
                            capture_lanes=None) -> SolveResult:
     """Batched newton_Algorithm over lanes x0 (B,4) sharing (x_ref, u_ref) -- or each with its own, x_ref (B,N,4) and
-    u_ref (B,N-1 or N,2) (serial / pipelined schedules) -- -> SolveResult (device tensors).
+    u_ref (B,N-1 or N,2) -- -> SolveResult (device tensors).
     ``hist_len`` keeps every lane's cost / max|sigma| history; ``capture_lanes`` keeps the listed lanes'
     trajectories after every accepted iteration (SolveResult.x_trajs, the reference's history['x_trajs'])."""
     return newton_solve_batch(x0, x_ref, u_ref, max_iters, tol=tol, beta=beta, c=c, gamma_0=gamma_0, max_ls=max_ls,
