@@ -270,7 +270,7 @@ class BatchedNewtonSolver:
         if self.persistent:
             self._run(k, k + 1)
         elif self.pipeline:
-            more =self.max_iters is None or k + 1 < self.max_iters
+            more = self.max_iters is None or k + 1 < self.max_iters
             self._phase(2 * k + 1, True)         # sweep H1 (iteration k) beside trial H0 (iteration k)
             self._phase(2 * k + 2, more)         # sweep H0 (iteration k+1) beside trial H1 (iteration k)
         else:
