@@ -16,7 +16,8 @@ value = lane-iterations executed by all ranks / max-over-ranks wall time  ("Newt
 states/s = value * T).  Prints ONE JSON line on rank 0.  Secondary legs timed in the same process and
 reported inside that line (--extra-legs): "strong_scaling_cfg4" (BASELINE cfg 4: 1,048,576 lanes
 strong-scaled over the N ranks) and, at N = 1, "general_path" (the same workload on the general kernels that
-stream the tau1 planes).  --workload cfg4 makes cfg 4 the main line; --workload mpc runs BASELINE cfg 5.
+stream the tau1 planes), "cfg2" (BASELINE cfg 2: 4,096 lanes) and "mpc_cfg5" (BASELINE cfg 5).  --workload cfg4
+makes cfg 4 the main line; --workload mpc makes cfg 5 the main line (with its CPU baseline).
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "swing-up Newton iterations/sec (batch×T states/s) at 1/2/4/8 MI355X"
 CFG4_LANES = 1048576           # BASELINE cfg 4: global lanes sharded over 8 GPUs
+CFG2_LANES = 4096              # BASELINE cfg 2: one GPU
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (datasheet)
 
@@ -106,32 +108,36 @@ def numpy_baseline(x0, x_ref, u_ref, lanes: int, iters: int):
 
 
 def run_mpc(a):
+    """--workload mpc: the cfg 5 line (mpc_line) printed as the bench's JSON line."""
+    print(json.dumps(mpc_line(a, a.batch, a.steps, a.warmup, a.cpu_lanes)), flush=True)
+
+
+def mpc_line(a, B, steps, warmup, cpu_lanes):
     """BASELINE cfg 5: batched receding-horizon MPC (trajectory_tracking.py:8-69 / main.py task_4).
 
-    One step = the whole tracking run of a.batch disturbed initial states: the exact per-control-step QP
-    solutions of all 500 windows (gym_tv_lqr_gains; horizon a.horizon) plus the batched closed-loop RK4
+    One step = the whole tracking run of B disturbed initial states: the exact per-control-step QP
+    solutions of all 500 windows (gym_mpc_gains; horizon a.horizon) plus the batched closed-loop RK4
     simulation under them (gym_track_rollout) and the lane-major results.  value = lanes x 500 control
-    steps / seconds per step."""
+    steps / seconds per step.  cpu_lanes = 0: no CPU baseline (the parity sample is then 256 lanes)."""
     import torch
     from gymnast_optimalcontrol_amd import trajectory_tracking as tt
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine  # noqa: F401
     g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))   # acrobot_optimal_trajectory
     x_ref, u_ref = g["x"], g["u"]
     N = x_ref.shape[0]
-    B = a.batch
     x0 = x_ref[0] + np.random.default_rng(0).uniform(-0.1, 0.1, (B, 4))
     x0[0] = x_ref[0] + 0.1                                      # main.task_4's disturbance
     eng = tt._eng()
     x0d, xrd, urd = eng.t(x0), eng.t(x_ref), eng.t(u_ref)
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         tt.solve_mpc_tracking_batch(x0d, xrd, urd, a.horizon)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         x, u, K0 = tt.solve_mpc_tracking_batch(x0d, xrd, urd, a.horizon)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.steps
-    steps = B * (N - 1)
+    dt = (time.perf_counter() - t0) / steps
+    ctrl_steps = B * (N - 1)
     # per-kernel times (HIP events on the engine's stream = torch's current stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     ev[0].record()
@@ -142,8 +148,8 @@ def run_mpc(a):
     torch.cuda.synchronize()
     t_gain, t_roll = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
     roll_bytes = B * (N * 32 + (N - 1) * 16 + 32)                 # x (pairs) + u (planes) written, x0 read
-    out = {"metric": "receding-horizon MPC control steps/s (BASELINE cfg 5)", "value": steps / dt,
-           "unit": "control steps/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * dt,
+    out = {"metric": "receding-horizon MPC control steps/s (BASELINE cfg 5)", "value": ctrl_steps / dt,
+           "unit": "control steps/s", "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * dt,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": f"cfg5: {B} disturbed initial states (x_ref[0] + U(-0.1,0.1)^4) x 500 control "
                                   f"steps, horizon {a.horizon}, exact QP solution per step, RK4 plant",
@@ -159,18 +165,19 @@ def run_mpc(a):
     if traffic is not None and B == 8192:
         out["roofline"].update({"traffic": traffic, "traffic_over_algorithmic": ratio, "traffic_source": src})
     from oracle import tracking_np as tr
-    lanes = min(B, a.cpu_lanes)
+    lanes = min(B, cpu_lanes or 256)
     t1 = time.perf_counter()
     xo, uo, K0o = tr.solve_mpc_tracking(x0[:lanes], x_ref, u_ref, a.horizon)
     tc = time.perf_counter() - t1
-    out["cpu_baseline"] = {"value": lanes * (N - 1) / tc, "unit": "control steps/s", "cores": 1, "kind": "port",
-                           "sample": f"first {lanes} lanes, numpy restatement (oracle/tracking_np.py) with the "
-                                     f"window QPs solved by the same Riccati recursion", "seconds": tc}
+    if cpu_lanes:
+        out["cpu_baseline"] = {"value": lanes * (N - 1) / tc, "unit": "control steps/s", "cores": 1, "kind": "port",
+                               "sample": f"first {lanes} lanes, numpy restatement (oracle/tracking_np.py) with the "
+                                         f"window QPs solved by the same Riccati recursion", "seconds": tc}
     xg = x[:lanes].cpu().numpy()
     out["parity"] = {"rel_l2_x_vs_oracle": float(np.linalg.norm(xg - xo) / np.linalg.norm(xo)),
                      "rel_l2_K0_vs_oracle": float(np.linalg.norm(K0.cpu().numpy() - K0o) / np.linalg.norm(K0o)),
-                     "lane0_final_state": x[0, -1].cpu().numpy().tolist(), "tolerance": 1e-9}
-    print(json.dumps(out), flush=True)
+                     "oracle_lanes": lanes, "lane0_final_state": x[0, -1].cpu().numpy().tolist(), "tolerance": 1e-9}
+    return out
 
 
 class NewtonLeg:
@@ -319,10 +326,11 @@ def main():
                     help="newton: the north-star metric (cfg 3 per GPU, weak scaling); cfg4: 1,048,576 lanes "
                          "strong-scaled over the ranks; mpc: BASELINE cfg 5; stress: the cfg 3 batch with "
                          "th ~ U(+-1.5) (SURVEY 8(d)'s stress variant: backtracking and Armijo failures)")
-    ap.add_argument("--extra-legs", default="cfg4,general",
+    ap.add_argument("--extra-legs", default="cfg4,general,cfg2,mpc",
                     help="comma list of secondary timed legs reported inside the same JSON line (newton "
                          "workload): cfg4 = 1,048,576 lanes strong-scaled over the ranks; general = the same "
-                         "workload on the general (tau1-streaming) kernels, N=1 only; '' for none")
+                         "workload on the general (tau1-streaming) kernels, N=1 only; cfg2 = BASELINE cfg 2 "
+                         "(4,096 lanes, N=1 only); mpc = BASELINE cfg 5 (N=1 only); '' for none")
     ap.add_argument("--extra-steps", type=int, default=2, help="timed solves of each extra leg (1 warmup)")
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
@@ -447,6 +455,23 @@ def main():
                     "as for any reference with a live tau1 channel such as task 1); bitwise-identical results "
                     "(tests/test_gpu_parity.py::test_u0_zero_stream_skipping_is_bitwise_identical)"}
         leg.free()
+
+    if "cfg2" in legs and world == 1 and (strong or a.batch != CFG2_LANES):
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG2_LANES, not a.no_timing).run(a.extra_steps, 1)
+        k2, r2 = leg.kernel_report(N)
+        out["cfg2"] = {
+            "value": leg.value, "unit": "Newton iterations/s", "lanes": CFG2_LANES, "steps": a.extra_steps,
+            "warmup": 1, "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
+            "roofline": None if r2 is None else {k: r2[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
+            "note": "BASELINE cfg 2: 4,096 lanes on one GPU (64 wavefronts of lanes on 1,024 SIMDs: latency-bound, "
+                    "the persistent schedule); --batch 4096 makes it the main line"}
+        leg.free()
+    if "mpc" in legs and world == 1:
+        m = mpc_line(a, 8192, max(a.extra_steps, 3), 1, 0)
+        out["mpc_cfg5"] = {k: m[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "kernels",
+                                             "roofline", "parity")}
+        out["mpc_cfg5"]["note"] = "BASELINE cfg 5 (--workload mpc makes it the main line, with its CPU baseline)"
 
     if rank == 0 and world == 1 and not a.no_cpu:
         x0_all = make_x0(total, spread=a.spread)
