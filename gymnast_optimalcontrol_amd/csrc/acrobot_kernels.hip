@@ -170,7 +170,7 @@ __device__ __forceinline__ void pin(double2 v) { asm volatile("" : : "v"(v.x), "
 
 // element index of (t, row p of P, lane) in a time-major plane stream (W = 1 doubles): (L, P, Bp)
 __device__ __forceinline__ int64_t pix(int t, int p, int P, int64_t l, int64_t Bp) { return ((int64_t)t * P + p) * Bp + l; }
-// Per-lane references (GYM_FLAG_REF_LANE, the serial schedule): x_ref (Bp, N, 4), u_ref (Bp, T, 2), lane-major.
+// Per-lane references (GYM_FLAG_REF_LANE, every schedule): x_ref (Bp, N, 4), u_ref (Bp, T, 2), lane-major.
 // RL kernels offset the reference pointers by the lane once; everything downstream reads stage t at +4t / +2t as
 // with the shared reference (then by vector instead of scalar loads: the same values, the same bits).
 template <bool RL>
@@ -2347,7 +2347,7 @@ struct TimedLaunch {  // records a start/stop event pair around one launch if th
     (((b)->flags & GYM_FLAG_U0_ZERO) ? (((b)->flags & GYM_FLAG_X_CKPT) ? kern<true, true> : kern<true, false>) \
                                      : (((b)->flags & GYM_FLAG_X_CKPT) ? kern<false, true> : kern<false, false>))
 
-// ... and, for the serial schedule's kernels, per-lane references (GYM_FLAG_REF_LANE; never with X_CKPT)
+// ... and per-lane references (GYM_FLAG_REF_LANE; never with X_CKPT), for the serial / pipelined kernels
 #define SERIAL_SEL(b, kern)                                                                                      \
     (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false, true>              \
                                                                           : kern<false, false, true>)           \
