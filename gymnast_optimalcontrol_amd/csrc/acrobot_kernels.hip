@@ -2515,15 +2515,17 @@ int gym_riccati_general(const double* A, const double* Bm, const double* Q, cons
     return launch_status();
 }
 
+// every batch entry point: the buffers, the sizes and the flag combination (per-lane references are never
+// combined with state checkpointing: no kernel instantiates both)
 static bool bad_batch(const gym_batch* b) {
     return !b || bad_dims(b->B, b->Bp, b->N) || !b->x[0] || !b->x[1] || !b->u[0] || !b->u[1] || !b->K1 || !b->cs ||
            !b->x_ref || !b->u_ref || !b->cost || !b->dJ || !b->smax || !b->gamma || !b->status || !b->n_iter ||
-           !b->res_buf || !b->n_roll || !b->retry_list || !b->counters || !b->partials || !b->stats;
+           !b->res_buf || !b->n_roll || !b->retry_list || !b->counters || !b->partials || !b->stats ||
+           ((b->flags & GYM_FLAG_REF_LANE) && (b->flags & GYM_FLAG_X_CKPT));
 }
 
 int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, const gym_batch* b, void* s) {
     if (!m || !w || !x0 || bad_batch(b)) return GYM_EINVAL;
-    if ((b->flags & GYM_FLAG_REF_LANE) && (b->flags & GYM_FLAG_X_CKPT)) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const int T = b->N - 1;
     hipError_t e = hipMemsetAsync(b->u[0], 0, sizeof(double) * 2 * (size_t)T * b->Bp, st);

@@ -78,6 +78,58 @@ def test_launchers_reject_bad_arguments_without_a_device():
     assert lib.gym_newton_init(None, None, None, C.byref(b), None) == 1
 
 
+def test_every_entry_point_rejects_null_pointers():
+    """The ABI's error contract (int status, no exceptions, no launch on bad arguments): every entry
+    point called with null pointers and otherwise plausible sizes returns GYM_EINVAL from its host-side checks."""
+    from gymnast_optimalcontrol_amd import _lib
+    lib = _lib.load()
+    for name, args in _lib._SIGS.items():
+        if name == "gym_abi_version":
+            continue
+        vals = [64 if a is C.c_int64 else 8 if a is C.c_int32 else 1e-6 if a is C.c_double else None for a in args]
+        assert getattr(lib, name)(*vals) == 1, name
+
+
+def test_batch_entry_points_reject_bad_sizes_and_flags():
+    """Batch sizes / horizons / flag combinations that no kernel supports are refused before any launch, by every
+    solver entry point.  (The buffers are dummy addresses: skipped where a device could run a launch.)"""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("dummy device addresses: CPU-only check")
+    from gymnast_optimalcontrol_amd import _lib
+    lib = _lib.load()
+    D = 0x10000
+    m, w, a = _lib.GymModel(dt=0.02), _lib.GymWeights(), _lib.GymArmijo(1e-4, 0.7, 0.5, 0.1, 20, 0)
+
+    def batch(B=64, Bp=64, N=501, flags=0):
+        b = _lib.GymBatch(B=B, Bp=Bp, N=N, flags=flags)
+        for f, t in _lib.GymBatch._fields_:
+            if f in ("x", "u"):
+                getattr(b, f)[0] = getattr(b, f)[1] = D
+            elif t is _lib._P and f not in ("hist_cost", "hist_smax", "lane_map"):
+                setattr(b, f, D)
+        return b
+
+    R = C.byref
+    for b in (batch(B=0), batch(B=65, Bp=64), batch(B=60, Bp=100), batch(N=1), batch(Bp=_lib.MAX_BP + 64),
+              batch(flags=_lib.FLAG_REF_LANE | _lib.FLAG_X_CKPT)):
+        rcs = [lib.gym_newton_init(R(m), R(w), D, R(b), None),
+               lib.gym_newton_iteration(R(m), R(w), R(a), R(b), 0, None),
+               lib.gym_newton_phase(R(m), R(w), R(a), R(b), 0, 1, None),
+               lib.gym_newton_run(R(m), R(w), R(a), R(b), 0, 1, None),
+               lib.gym_newton_sigma(R(m), R(w), R(b), D, None),
+               lib.gym_newton_fill_states(R(m), R(b), 0, None),
+               lib.gym_newton_finalize(R(m), R(w), R(b), 1, D, D, D, D, None),
+               lib.gym_newton_gamma_sweep(R(m), R(w), R(a), R(b), 0, D, 4, D, None)]
+        assert rcs == [1] * 8, (b.B, b.Bp, b.N, b.flags, rcs)
+    b = batch()
+    assert lib.gym_newton_run(R(m), R(w), R(a), R(b), 5, 1, None) == 1                   # k1 < k0
+    assert lib.gym_newton_iteration(R(m), R(w), R(_lib.GymArmijo(1e-4, 0.7, 0.5, 0.1, 0, 0)), R(b), 0, None) == 1
+    assert lib.gym_rk4_step(R(m), D, D, D, -1, None) == 1 and lib.gym_jacobians(R(m), D, D, D, D, -1, None) == 1
+    assert lib.gym_track_rollout(R(m), D, D, D, D, -1, 500, D, D, None) == 1
+    assert lib.gym_mpc_gains(R(m), D, D, 501, D, D, D, D, 300, 10, 100, 1e-6, D, D, D, None) == 1  # L + 2 > 256
+
+
 def test_shard_range_partitions_exactly():
     from gymnast_optimalcontrol_amd.distributed import shard_range
     for total in (1, 7, 64, 1000, 1048576):
