@@ -72,10 +72,10 @@ class BatchedNewtonSolver:
     # overlap).  In units of lanes per compute unit (4 SIMDs x 64 lanes x 1.25).
     PIPELINE_MIN_LANES_PER_CU = 320
     # The persistent schedule (one launch per solve: no per-iteration launches, statistics or host round trips)
-    # is ahead while the batch is latency-bound well below one wavefront per SIMD (same-box A/B: +16% at 4,096
-    # lanes = BASELINE cfg 2, +10% at 16,384, +4% at 24,576, even at 32,768, 10% behind serial at 65,536;
-    # profiles/r01_ab_persistent.log).
-    PERSISTENT_MAX_LANES_PER_CU = 96
+    # is ahead while the batch is latency-bound: its four-wavefront kernel (k_nt_run2) measured +59% over serial
+    # at 16,384 lanes, +10% at 24,576, +5.5% at 32,768 (= 2 workgroups per CU), and 10% behind from 36,864 on,
+    # where some CUs take a third workgroup (same box, profiles/r02_sched_sweep.log).
+    PERSISTENT_MAX_LANES_PER_CU = 128
 
     @staticmethod
     def pipeline_min_lanes(device) -> int:

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Throughput of both solver schedules at small batch sizes (measurement tool).
+# Throughput of the solver schedules at the given batch sizes (measurement tool); SCHEDS selects them.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 for b in "$@"; do
-  for s in serial pipelined; do
-    timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu --batch $b --schedule $s > gpurun_out/sched_${b}_$s.log 2>&1
+  for s in ${SCHEDS:-serial pipelined persistent}; do
+    timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu --extra-legs '' --batch $b --schedule $s > gpurun_out/sched_${b}_$s.log 2>&1
     rc=$?
     python3 - "$b" "$s" <<'PY'
 import json, re, sys
