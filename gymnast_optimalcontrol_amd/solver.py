@@ -66,11 +66,11 @@ class SolveResult:
 class BatchedNewtonSolver:
     """Owns the device buffers of a batch of ``B`` lanes that share x_ref / u_ref."""
 
-    # The pipelined schedule pays off once the batch is more than ~1.25 wavefronts per SIMD (measured on one
-    # MI355X, profiles/r01_batch_sweep.log: serial is ahead up to 65,536 lanes = 1 wave/SIMD, pipelined from
-    # 98,304 on; below that the solve is latency-bound and the two phases per iteration cost more than they
-    # overlap).  In units of lanes per compute unit (4 SIMDs x 64 lanes x 1.25).
-    PIPELINE_MIN_LANES_PER_CU = 320
+    # The pipelined schedule pays off once the batch holds two wavefronts per SIMD: with the round-2 kernels
+    # serial is ahead by 2% at 73,728 and 81,920 lanes and by 1% at 98,304, the two are level (+-1%, box
+    # dependent) from 131,072 to 327,680 (same-box sweeps, profiles/r02_sched_sweep_large.log; round 1's
+    # kernels crossed at ~81,920, profiles/r01_batch_sweep.log).  In lanes per compute unit (4 SIMDs x 64 x 2).
+    PIPELINE_MIN_LANES_PER_CU = 512
     # The persistent schedule (one launch per solve: no per-iteration launches, statistics or host round trips)
     # is ahead while the batch is latency-bound: its four-wavefront kernel (k_nt_run2) measured +59% over serial
     # at 16,384 lanes, +10% at 24,576, +5.5% at 32,768 (= 2 workgroups per CU), and 10% behind from 36,864 on,
