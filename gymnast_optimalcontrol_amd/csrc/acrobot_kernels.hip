@@ -371,9 +371,12 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
 // Stage t's linearisation (build_stage_lists :166-181 with discretize_linearization :161-164): rows 2, 3 of
 // A_d = I + dt A_c (rows 0, 1 are [1 0 dt 0], [0 1 0 dt]), column 1 of B_d = dt B_c, q_t = 2Q dx_t, r_t = 2R du_t.
 // A function of x_t, u_t only (not of P), so it can be evaluated apart from the Riccati chain.
+// U0Z (GYM_FLAG_U0_ZERO: u0 = ur0 = 0): r0 = 2R0 (u0 - ur0) is +0 (the bits the general expression gives), and the
+// Riccati step drops the terms it zeroes (sigma0 = -0, its dJ and max|sigma| contributions): the same bits.
 struct Lin {
     double A20, A21, A22, A23, A30, A31, A32, A33, bd2, bd3, q0, q1, q2, q3, r0, r1, dt;
 };
+template <bool U0Z = false>
 __device__ __forceinline__ Lin stage_lin(const Dyn& m, const KW& w, const gym::Jac& J, double2 xa, double2 xb,
                                          double ut0, double ut1, const double* xrt, const double* urt) {
 #pragma clang fp contract(on)
@@ -384,7 +387,8 @@ __device__ __forceinline__ Lin stage_lin(const Dyn& m, const KW& w, const gym::J
     L.bd2 = dt * J.bc2; L.bd3 = dt * J.bc3;
     L.q0 = w.twoQ[0] * (xa.x - xrt[0]); L.q1 = w.twoQ[1] * (xa.y - xrt[1]);
     L.q2 = w.twoQ[2] * (xb.x - xrt[2]); L.q3 = w.twoQ[3] * (xb.y - xrt[3]);
-    L.r0 = w.G00 * (ut0 - urt[0]); L.r1 = w.twoR1 * (ut1 - urt[1]);
+    L.r0 = U0Z ? 0.0 : w.G00 * (ut0 - urt[0]);
+    L.r1 = w.twoR1 * (ut1 - urt[1]);
     L.dt = dt;
     return L;
 }
@@ -405,20 +409,23 @@ struct Sweep {
     }
 
     // stage t (x_t = (xa, xb), u_t = (ut0, ut1)): gain row 1 k[0..3], sigma (s0, s1); updates P, p, dJ, smax
+    template <bool U0Z = false>
     __device__ __forceinline__ void step(const Dyn& m, const KW& w, double2 xa, double2 xb, double ut0, double ut1,
                                          const double* xrt, const double* urt, double& k0, double& k1,
                                          double& k2, double& k3, double& s0, double& s1,
                                          const gym::PolyRegs& pk = gym::poly_lits()) {
-        step_j(m, w, gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1, pk), xa, xb, ut0, ut1, xrt, urt, k0, k1, k2, k3,
-               s0, s1);
+        step_j<U0Z>(m, w, gym::jacobian(m, xa.x, xa.y, xb.x, xb.y, ut1, pk), xa, xb, ut0, ut1, xrt, urt, k0, k1, k2,
+                    k3, s0, s1);
     }
     // the same with the stage's Jacobian already evaluated (it depends on x_t, u_t only, not on P)
+    template <bool U0Z = false>
     __device__ __forceinline__ void step_j(const Dyn& m, const KW& w, const gym::Jac& J, double2 xa, double2 xb,
                                            double ut0, double ut1, const double* xrt, const double* urt, double& k0,
                                            double& k1, double& k2, double& k3, double& s0, double& s1) {
-        step_lin(w, stage_lin(m, w, J, xa, xb, ut0, ut1, xrt, urt), k0, k1, k2, k3, s0, s1);
+        step_lin<U0Z>(w, stage_lin<U0Z>(m, w, J, xa, xb, ut0, ut1, xrt, urt), k0, k1, k2, k3, s0, s1);
     }
     // the Riccati update of stage t from its linearisation (stage_lin: a function of x_t, u_t only)
+    template <bool U0Z = false>
     __device__ __forceinline__ void step_lin(const KW& w, const Lin& L, double& k0, double& k1, double& k2,
                                              double& k3, double& s0, double& s1) {
         // FMA contraction within each expression only, never across statements: the bits then do not depend on
@@ -449,8 +456,15 @@ struct Sweep {
         const double g1 = r1 + (bd2 * p2 + bd3 * p3);
         const double iG = 1.0 / G11;
         k0 = -F0 * iG; k1 = -F1 * iG; k2 = -F2 * iG; k3 = -F3 * iG;
-        s0 = -r0 * w.iG00; s1 = -g1 * iG;
-        dJ += r0 * s0 + g1 * s1;
+        s1 = -g1 * iG;
+        if (U0Z) {   // r0 = +0: sigma0 = -0, and r0 sigma0 + g1 sigma1 = g1 sigma1 exactly
+            s0 = -0.0;
+            const double d1 = g1 * s1;
+            dJ += d1;
+        } else {
+            s0 = -r0 * w.iG00;
+            dJ += r0 * s0 + g1 * s1;
+        }
         // W = P A_d
         const double W00 = P00 + P02 * A20 + P03 * A30, W01 = P01 + P02 * A21 + P03 * A31;
         const double W02 = dt * P00 + P02 * A22 + P03 * A32, W03 = dt * P01 + P02 * A23 + P03 * A33;
@@ -481,7 +495,8 @@ struct Sweep {
         P00 = nP00; P01 = nP01; P02 = nP02; P03 = nP03; P11 = nP11; P12 = nP12; P13 = nP13;
         P22 = nP22; P23 = nP23; P33 = nP33;
         p0 = np0; p1 = np1; p2 = np2; p3 = np3;
-        smax = gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
+        // U0Z: |sigma0| = 0 never raises smax (>= 0 or NaN)
+        smax = U0Z ? gym::nanmax_abs(smax, s1) : gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
     }
 };
 
@@ -587,7 +602,7 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         }
         double k0, k1, k2, k3, s0, s1;
         const KArgs ka = kernarg_consts();   // the kernel's (Dyn, KW) arguments, re-read: no SGPR spills
-        S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
+        S.step<U0Z>(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1, pk);
         store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, xa, xb, ut1, g0, k0, k1, k2, k3, s1);
     }
     dJ_out = S.dJ;
@@ -639,7 +654,7 @@ __device__ __forceinline__ void backward_solver_lane_ilp(const Dyn& m, const KW&
         if (t >= 1) Jn = jac(n);
         double k0, k1, k2, k3, s0, s1;
         const KArgs ka = kernarg_consts();
-        S.step_j(ka.m, ka.w, Jc, c.xa, c.xb, c.u0, c.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+        S.step_j<U0Z>(ka.m, ka.w, Jc, c.xa, c.xb, c.u0, c.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
         store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, c.xa, c.xb, c.u1, g0, k0, k1, k2, k3, s1);
     };
     SweepStage A, B, C;
@@ -747,7 +762,7 @@ __device__ __forceinline__ void backward_solver_lane_ck(const Dyn& m, const KW& 
                 const double ut1 = lu1[j * BLK + ln], ut0 = U0Z ? 0.0 : lu0[j * BLK + ln];
                 double k0, k1, k2, k3, s0, s1;
                 const KArgs ka = kernarg_consts();
-                S.step(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
+                S.step<U0Z>(ka.m, ka.w, xa, xb, ut0, ut1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1);
                 store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, xa, xb, ut1, g0, k0, k1, k2, k3, s1);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -1772,7 +1787,7 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
         const gym::Jac J = gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
         const Row<4> xrt = ref_row<4, RL>(xr, t);
         const Row<2> urt = ref_row<2, RL>(ur, t);
-        const Lin L = stage_lin(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
+        const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
         double2(*s)[BLK] = ring[slot];
         s[0][lane] = q.xa;                          s[1][lane] = q.xb;
         s[2][lane] = make_double2(q.u0, q.u1);      s[3][lane] = make_double2(L.A20, L.A21);
@@ -1838,7 +1853,7 @@ __device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l
                 const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
                             qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
                 double k0, k1, k2, k3, s0, s1;
-                S.step_lin(ka.w, L, k0, k1, k2, k3, s0, s1);
+                S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
                 if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, k0, k1, k2,
                                                  k3, s1);
             }

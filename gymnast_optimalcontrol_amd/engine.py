@@ -32,6 +32,10 @@ class Weights:
     QT: tuple = QT_DIAG
 
     def c_struct(self) -> _lib.GymWeights:
+        # R > 0: the reference's G = R_t + B^T P B is diag(2 R0, .) with B[:, 0] = 0, and np.linalg.solve raises on
+        # a singular G (trajectory_generation.py:203-204); the kernels divide by 2 R0 and 2 R1 + b^T P b
+        if not all(np.isfinite(v) and v > 0 for v in self.R):
+            raise ValueError(f"R must be positive (G = diag(2 R0, 2 R1 + b^T P b) is inverted), got {self.R}")
         w = _lib.GymWeights()
         w.Q[:] = [float(v) for v in self.Q]
         w.R[:] = [float(v) for v in self.R]

@@ -152,6 +152,10 @@ def test_weights_from_matrices():
     with pytest.raises(ValueError):
         Weights.from_matrices(np.eye(3), np.eye(2), np.eye(4))
     assert [padded(b) for b in (1, 64, 65, 4096)] == [64, 64, 128, 4096]
+    for bad in ((0.0, 1.5), (1e-6, -1.0), (float("nan"), 1.5)):    # singular / invalid G (reference: LinAlgError)
+        with pytest.raises(ValueError):
+            Weights(R=bad).c_struct()
+    assert Weights().c_struct().R[1] == 1.5
 
 
 def test_product_fails_loudly_without_device():
