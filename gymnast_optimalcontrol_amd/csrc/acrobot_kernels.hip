@@ -197,12 +197,19 @@ __device__ __forceinline__ double xcost(const double* w, double n0, double n1, d
     return ((e0 * (w[0] * e0) + e1 * (w[1] * e1)) + e2 * (w[2] * e2)) + e3 * (w[3] * e3);
 }
 // one stage of total_cost (:244-245) added to the running J, with FMA contraction inside each expression only:
-// the same bits in every kernel that accumulates a trial's cost
+// the same bits in every kernel that accumulates a trial's cost.  U0Z: f0 = +0, so f0 (R0 f0) + f1 (R1 f1) is
+// f1 (R1 f1) exactly (both contractions of the general expression round to it)
+template <bool U0Z = false>
 __device__ __forceinline__ double stage_cost(double J, const double* Q, const double* R, double n0, double n1,
                                             double n2, double n3, const double* xrt, double f0, double f1) {
 #pragma clang fp contract(on)
     J += xcost(Q, n0, n1, n2, n3, xrt);
-    J += f0 * (R[0] * f0) + f1 * (R[1] * f1);
+    if (U0Z) {
+        const double c1 = f1 * (R[1] * f1);
+        J += c1;
+    } else {
+        J += f0 * (R[0] * f0) + f1 * (R[1] * f1);
+    }
     return J;
 }
 
@@ -331,12 +338,12 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     auto body = [&](const TrialStage& q, int t) {
         prio_band<BAND ? 1 : PRIO_NONE>(t, T);
         const double* urt = ur + 2 * t;
-        const double v0 = trial_u0(q.u0, urt[0], gamma, G00, iG00);
+        const double v0 = U0Z ? 0.0 : trial_u0(q.u0, urt[0], gamma, G00, iG00);   // U0Z: +0 exactly
         const double v1 = SIG ? trial_u1_sig(q.k0, q.k1, q.cg, q.s1, dg, n0, n1, n2, n3)
                               : trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
-        const double f0 = v0 - urt[0], f1 = v1 - urt[1];
+        const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
-        J = stage_cost(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
+        J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
             if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
@@ -2010,10 +2017,10 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
                 const Row<4> xrt = ref_row<4, RL>(xr, t);
                 const KArgs ka = kernarg_consts();
                 const double u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
-                const double v0 = trial_u0(u0, urt.v[0], gamma, ka.w.G00, ka.w.iG00);
+                const double v0 = U0Z ? 0.0 : trial_u0(u0, urt.v[0], gamma, ka.w.G00, ka.w.iG00);
                 const double v1 = vv.x;
-                const double f0 = v0 - urt.v[0], f1 = v1 - urt.v[1];
-                J = stage_cost(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
+                const double f0 = U0Z ? 0.0 : v0 - urt.v[0], f1 = v1 - urt.v[1];
+                J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
                 if (act) {
                     const auto rO = rsrc(Ob + (int64_t)t * row);
                     if (!U0Z) bst1(rO, o1, 0, v0);
