@@ -461,7 +461,7 @@ struct Sweep {
         const double F2 = dt * Pb0 + A22 * Pb2 + A32 * Pb3;
         const double F3 = dt * Pb1 + A23 * Pb2 + A33 * Pb3;
         const double g1 = r1 + (bd2 * p2 + bd3 * p3);
-        const double iG = 1.0 / G11;
+        const double iG = gym::recip(G11);   // G11 = 2 R1 + b^T P b >= 2 R1 > 0: rcp + two Newton steps
         k0 = -F0 * iG; k1 = -F1 * iG; k2 = -F2 * iG; k3 = -F3 * iG;
         s1 = -g1 * iG;
         if (U0Z) {   // r0 = +0: sigma0 = -0, and r0 sigma0 + g1 sigma1 = g1 sigma1 exactly
