@@ -2567,6 +2567,15 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
     return launch_status();
 }
 
+// Grid caps of the post-trial kernels (grid-stride over the retry list; any cap is correct).  They launch every
+// phase, also when no lane rejected trial 1 (the device-side count is not known to the host); measurement
+// variants lower them.
+#ifndef GYM_POST_CAP
+#define GYM_POST_CAP 2048
+#endif
+#ifndef GYM_CAND_CAP
+#define GYM_CAND_CAP 4096
+#endif
 static void launch_post_trial(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                               const SolverCtl& c, const TrialIO& io, Range rg, int32_t* counter, double* stats_out,
                               const double* other, double* total, hipStream_t st) {
@@ -2577,18 +2586,18 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
     if (a->max_ls > 1 && n > 0) {
         {   // the lanes that reject trial 1 need sigma1: re-run their sweep of this iteration into its plane
             TimedLaunch tl(b->timing, 7, st);
-            hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m),
+            hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, GYM_POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
                                kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
                                (const int32_t*)nullptr, -1, b->B, b->Bp, b->N);
         }
         {
             TimedLaunch tl(b->timing, 2, st);
-            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, 4096);
+            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, GYM_CAND_CAP);
             hipLaunchKernelGGL(CAND_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
                                b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, 2048)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, GYM_POST_CAP)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
                            b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
                            b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
     }

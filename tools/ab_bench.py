@@ -26,13 +26,14 @@ def main():
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--max-iters", type=int, default=5000)
+    ap.add_argument("--spread", type=float, default=0.5, help="th0 ~ U(+-spread) (1.5: the stress workload)")
     a = ap.parse_args()
     import torch
     from bench import load_refs, make_x0
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
     x_ref, u_ref = load_refs()
-    x0 = make_x0(a.batch)
+    x0 = make_x0(a.batch, spread=a.spread)
     from gymnast_optimalcontrol_amd import _lib
     def split(spec):
         path, *opts = spec.split(":")
