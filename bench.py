@@ -5,6 +5,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher (WORLD_SIZE unset) and N > 1, bench.py starts its N ranks itself: the parent makes no HIP
+call, spawns N child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and exits with the first
+non-zero child status.  Under a launcher WORLD_SIZE must equal --gpus, or the run exits with status 2.
+
 One *step* = one complete batched solve (newton_Algorithm semantics per lane, task-2 settings:
 tol 1e-4, gamma_0 0.1, beta 0.7, c 0.5, <= 20 Armijo trials, max_iters 5000) of this rank's shard
 of synthetic lanes, from u = 0 to every lane converged / failed, with inputs resident in HBM.
@@ -24,6 +28,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -302,6 +308,37 @@ def pmc_traffic(dom: str):
     return traffic, ratio, valu, src
 
 
+def spawn_ranks(n: int) -> int:
+    """Run this script as ``n`` ranks on one node (the torch.distributed.run equivalent), from a parent that has
+    made no HIP call: children are started with fork + exec of a fresh interpreter.  Returns the exit status
+    (0, or the first failing rank's; the other ranks are then terminated by PID)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   GYM_BENCH_LAUNCHER="bench.py (spawned ranks)")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with status {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -339,12 +376,26 @@ def main():
                     help="persistent schedule: iterations per launch (0: all of max_iters in one)")
     ap.add_argument("--split-waves", choices=("on", "off"), default="on",
                     help="persistent schedule: two wavefronts per 64 lanes (k_nt_run2, default) or one (k_nt_run)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rendezvous check only (no GPU work): every rank joins the process group and "
+                         "rank 0 prints the ranks' view of it as one JSON line")
     ap.add_argument("--u0-zero", choices=("auto", "off"), default="auto",
                     help="off: force the general kernels (tau1 planes streamed) for the main leg")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))         # before any torch / HIP call in this process
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
+        sys.exit(2)
     if a.batch is None:
         a.batch = 8192 if a.workload == "mpc" else 262144
     if a.workload == "mpc":
+        if a.gpus > 1:
+            print("bench.py: --workload mpc runs on one GPU (--gpus 1)", file=sys.stderr)
+            sys.exit(2)
         return run_mpc(a)
     if a.workload == "cfg4" and a.global_batch is None:
         a.global_batch = CFG4_LANES
@@ -353,8 +404,24 @@ def main():
     import torch
     from gymnast_optimalcontrol_amd import distributed as gd
     rank, local_rank, world = gd.init_process_group()
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if gd.rank_world()[1] != world or world != a.gpus:
+        print(f"bench.py: process group holds {gd.rank_world()[1]} ranks, expected {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if a.dry_run:
+        seen = [rank, world, os.getpid()]
+        backend = gd.backend_name()
+        if world > 1:
+            import torch.distributed as dist
+            parts = [None] * world
+            dist.all_gather_object(parts, seen)
+            dist.destroy_process_group()
+        else:
+            parts = [seen]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "dist": {"backend": backend,
+                              "world_size": world, "launcher": os.environ.get("GYM_BENCH_LAUNCHER")},
+                              "ranks": [p[0] for p in parts], "pids": [p[2] for p in parts]}), flush=True)
+        return
     torch.cuda.set_device(gd.local_device_index(local_rank))
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
 
@@ -406,7 +473,9 @@ def main():
            "config": {"workload": label + f", T={T}, fp64, task-2 Newton/Armijo settings, solved to convergence",
                       "lanes_per_gpu": per_gpu, "global_lanes": total, "horizon_T": T,
                       "parallelism": f"lane-sharded x{world} (1 all-reduce of 8 fp64 stats per host sync)"},
-           "states_per_s": value * T}
+           "states_per_s": value * T,
+           "dist": {"backend": gd.backend_name(), "world_size": gd.rank_world()[1],
+                    "launcher": os.environ.get("GYM_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else None)}}
     out["rollouts_per_s"] = main_leg.rollouts_all / main_leg.elapsed   # closed-loop Armijo rollouts, all ranks
 
     kern, roof = main_leg.kernel_report(N)

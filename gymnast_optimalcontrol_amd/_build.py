@@ -7,6 +7,7 @@ the working tree.  Nothing here ever falls back to a CPU implementation.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -21,6 +22,34 @@ LIB_PATH = os.path.join(PKG, LIB_NAME)
 SOURCES = [os.path.join(CSRC, "acrobot_kernels.hip"), os.path.join(CSRC, "tracking_kernels.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "acrobot_device.hpp"), os.path.join(INCLUDE, "gymnast_acrobot.h")]
 ARCH = os.environ.get("GYM_OFFLOAD_ARCH", "gfx950")
+BUILD_ID_TAG = b"gym-build-id:"      # marker in front of the id string inside the library's .rodata
+
+
+def source_hash() -> str:
+    """Build id of the tree: sha256 over the kernel sources and the ABI header (names and contents), 16 hex
+    digits.  The library embeds the id it was compiled from (gym_build_id); _lib.load refuses a mismatch, so a
+    stale libgymnast_acrobot.so that travelled with the tree can never run silently against newer sources."""
+    h = hashlib.sha256()
+    for p in sorted(DEPS):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def embedded_build_id(path: str = LIB_PATH) -> str | None:
+    """The build id compiled into the library file at ``path`` (read from the file, nothing is loaded)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_TAG)
+    if i < 0:
+        return None
+    raw = data[i + len(BUILD_ID_TAG): i + len(BUILD_ID_TAG) + 16]
+    return raw.decode("ascii", "replace")
 
 
 def hipcc() -> str:
@@ -31,10 +60,8 @@ def hipcc() -> str:
 
 
 def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in DEPS)
+    """Rebuild unless the library's embedded build id is the tree's source hash (contents, not mtimes)."""
+    return embedded_build_id(LIB_PATH) != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
@@ -44,7 +71,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
         return LIB_PATH
     tmp = target + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           *[f"-D{d}" for d in defines], "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
+           f"-DGYM_BUILD_ID=\"{source_hash()}\"", *[f"-D{d}" for d in defines], "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

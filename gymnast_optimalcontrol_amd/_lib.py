@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("GYM_LIB_PATH") or _build.LIB_PATH
 
 # exported symbols, in include/gymnast_acrobot.h order (tests check every one is present)
 EXPORTS = (
-    "gym_abi_version", "gym_model_from_params",
+    "gym_abi_version", "gym_build_id", "gym_model_from_params",
     "gym_continuous_dynamics", "gym_rk4_step", "gym_jacobians", "gym_stage_cost_derivs",
     "gym_pack_lanes", "gym_unpack_lanes", "gym_unpack_gains",
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
@@ -30,7 +30,7 @@ EXPORTS = (
 )
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run")
 
-ABI_VERSION = 9         # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 10        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
@@ -127,6 +127,12 @@ def load(path: str = LIB_PATH):
         if lib.gym_abi_version() != ABI_VERSION:
             raise ImportError(f"{path} implements ABI {lib.gym_abi_version()}, this binding needs {ABI_VERSION}: "
                               "rebuild the HIP library")
+        lib.gym_build_id.restype = C.c_char_p
+        lib.gym_build_id.argtypes = []
+        have, want = lib.gym_build_id().decode(), _build.source_hash()
+        if have != want and not os.environ.get("GYM_ALLOW_FOREIGN_BUILD"):
+            raise ImportError(f"{path} was built from other sources (build id {have}, tree {want}): stale binary, "
+                              "rebuild it (__graft_entry__.build() or python -m gymnast_optimalcontrol_amd._build)")
         for name, args in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = args

@@ -2415,6 +2415,14 @@ extern "C" {
 
 int gym_abi_version(void) { return GYM_ABI_VERSION; }
 
+// _build.source_hash() of the sources this library was compiled from (-DGYM_BUILD_ID); the tag lets the build
+// script read it from the file without loading the library
+#ifndef GYM_BUILD_ID
+#define GYM_BUILD_ID "unversioned"
+#endif
+static const char gym_build_id_tagged[] = "gym-build-id:" GYM_BUILD_ID;
+const char* gym_build_id(void) { return gym_build_id_tagged + sizeof("gym-build-id:") - 1; }
+
 int gym_model_from_params(const double p[11], double dt, gym_model* out) {
     if (!p || !out) return GYM_EINVAL;
     const double m1 = p[0], m2 = p[1], l1 = p[2], lc1 = p[3], lc2 = p[5], I1 = p[6], I2 = p[7], g = p[8];

@@ -4,7 +4,12 @@ Trajectories are independent, so the batch is partitioned into contiguous shards
 data-path collective.  The only exchange is one SUM all-reduce per outer iteration of the 8
 solver statistics (solver.STAT_FIELDS: active lanes, sum of J, sum of max|sigma|^2, ...), which
 gives every rank the global stop condition and the global cost / descent-norm scalars.  The
-message is 64 bytes, so it is latency-bound; it is issued on the solver's stream.
+message is 64 bytes, so it is latency-bound.  It is enqueued from the solver's stream (the engine
+launches on torch's current stream, and RCCL's communication stream waits on it), so it orders after
+the iteration's statistics kernel without a host synchronisation.
+
+``force=True`` (every collective helper here) runs the collective even on a 1-rank group: RCCL refuses two
+ranks on one device, so that is how a one-GPU box executes the device-tensor RCCL branches the 8-GPU run uses.
 """
 from __future__ import annotations
 
@@ -37,6 +42,13 @@ def rank_world(group=None) -> tuple[int, int]:
     return 0, 1
 
 
+def backend_name(group=None) -> str | None:
+    """The process group's backend ("nccl" = RCCL, "gloo"), or None for a single process without a group."""
+    if dist.is_available() and dist.is_initialized():
+        return str(dist.get_backend(group))
+    return None
+
+
 def local_device_index(local_rank: int) -> int:
     """This rank's GPU: local_rank, wrapped onto the visible devices (one process per GPU on a full node; a
     multi-rank rehearsal on fewer GPUs shares them)."""
@@ -44,27 +56,34 @@ def local_device_index(local_rank: int) -> int:
     return local_rank % n if n else 0
 
 
-def init_process_group(backend: str | None = None):
-    """Initialise torch.distributed from the environment if WORLD_SIZE > 1 (RCCL on GPUs, gloo on CPU).
+def init_process_group(backend: str | None = None, force: bool = False):
+    """Initialise torch.distributed from the environment if WORLD_SIZE > 1 (RCCL on GPUs, gloo on CPU), or at
+    any world size with ``force`` (a 1-rank group: exercises the collective path on one GPU).
 
     GYM_DIST_BACKEND overrides the backend (e.g. gloo to rehearse several ranks on one GPU: RCCL refuses two
     ranks on the same device)."""
     rank, local_rank, world = env_rank_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         backend = backend or os.environ.get("GYM_DIST_BACKEND")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local_device_index(local_rank))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
         kw = {"device_id": torch.device("cuda", local_device_index(local_rank))} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, local_rank, world
 
 
-def make_reduce_stats(group=None):
-    """SUM all-reduce of the per-iteration statistics, or None when running a single process."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+def _collective(group, force: bool) -> bool:
+    """Whether the helpers below run a collective: a process group exists and holds several ranks (or force)."""
+    return dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1)
+
+
+def make_reduce_stats(group=None, force: bool = False):
+    """SUM all-reduce of the per-iteration statistics, or None when running a single process (unless force)."""
+    if not _collective(group, force):
         return None
     backend = dist.get_backend(group)
 
@@ -83,9 +102,9 @@ def barrier(group=None):
         dist.barrier(group=group)
 
 
-def max_over_ranks(value: float, group=None) -> float:
+def max_over_ranks(value: float, group=None, force: bool = False) -> float:
     """Max of a host scalar over ranks (timing: the job's time is its slowest rank's)."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not _collective(group, force):
         return float(value)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
     t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
@@ -93,8 +112,8 @@ def max_over_ranks(value: float, group=None) -> float:
     return float(t.item())
 
 
-def sum_over_ranks(value: float, group=None) -> float:
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+def sum_over_ranks(value: float, group=None, force: bool = False) -> float:
+    if not _collective(group, force):
         return float(value)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
     t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
@@ -103,14 +122,16 @@ def sum_over_ranks(value: float, group=None) -> float:
 
 
 def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool = False, gather: bool = False,
-                  **solver_kw):
+                  force_collectives: bool = False, **solver_kw):
     """Solve this rank's contiguous shard of ``x0_all`` (B_total,4); stop on the GLOBAL active count.
 
     Every rank must hold a non-empty shard (``len(x0_all) >= world``; checked on every rank before any
     collective, so all of them raise together).  The automatic schedule is chosen on the largest shard
     (``schedule_lanes``), so every rank runs the same schedule and issues its all-reduces at the same
     iterations.  Returns (lo, hi, SolveResult of the local shard); with ``gather=True`` the third item is instead
-    the dict of global per-lane results (``gather_sharded`` of GATHER_FIELDS) on every rank."""
+    the dict of global per-lane results (``gather_sharded`` of GATHER_FIELDS) on every rank.  Per-lane references
+    (x_ref (B_total,N,4), u_ref (B_total,T,2)) are cut to the rank's shard.  ``force_collectives`` runs the
+    all-reduce / all-gather even on a 1-rank group."""
     from .engine import AcrobotEngine
     from .solver import BatchedNewtonSolver
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -119,24 +140,30 @@ def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool
     lo, hi = shard_range(total, rank, world)
     if total < world:
         raise ValueError(f"{total} lanes cannot be sharded over {world} ranks (every rank needs one)")
+    if np.ndim(x_ref) == 3:       # per-lane references: this rank's rows only
+        if len(x_ref) != total or len(u_ref) != total:
+            raise ValueError(f"per-lane references must hold {total} lanes, got {len(x_ref)} / {len(u_ref)}")
+        x_ref, u_ref = x_ref[lo:hi], u_ref[lo:hi]
     eng = engine or AcrobotEngine()
     solver_kw.setdefault("schedule_lanes", schedule_lanes(total, world))
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **solver_kw)
-    res = solver.solve(np.asarray(x0_all)[lo:hi], max_iters, reduce_stats=make_reduce_stats(), keep_stats=keep_stats)
+    x0_loc = x0_all[lo:hi] if isinstance(x0_all, torch.Tensor) else np.asarray(x0_all)[lo:hi]
+    res = solver.solve(x0_loc, max_iters, reduce_stats=make_reduce_stats(force=force_collectives),
+                       keep_stats=keep_stats)
     if gather:
-        return lo, hi, gather_sharded({f: getattr(res, f) for f in GATHER_FIELDS}, total)
+        return lo, hi, gather_sharded({f: getattr(res, f) for f in GATHER_FIELDS}, total, force=force_collectives)
     return lo, hi, res
 
 
 GATHER_FIELDS = ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma")
 
 
-def gather_sharded(local: dict, total: int, group=None) -> dict:
+def gather_sharded(local: dict, total: int, group=None, force: bool = False) -> dict:
     """The global per-lane results on every rank from each rank's contiguous shard ("ship the final
     per-lane outputs with an all-gather ... only if requested"): ``local`` maps a name to this rank's
     (hi - lo, ...) tensor; returns name -> (total, ...) tensors in lane order.  Ragged shards are padded to the
     largest one for the collective (RCCL all-gather on device tensors; gloo moves them through the host)."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not _collective(group, force):
         return dict(local)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     lo, hi = shard_range(total, rank, world)

@@ -31,11 +31,20 @@ class Weights:
     R: tuple = R_DIAG
     QT: tuple = QT_DIAG
 
-    def c_struct(self) -> _lib.GymWeights:
-        # R > 0: the reference's G = R_t + B^T P B is diag(2 R0, .) with B[:, 0] = 0, and np.linalg.solve raises on
-        # a singular G (trajectory_generation.py:203-204); the kernels divide by 2 R0 and 2 R1 + b^T P b
+    def require_gain_solvable(self):
+        """Checked wherever G is inverted (the solver, the gain sweeps; cost-only paths accept any weights, as the
+        reference does).  R > 0: the reference's G = R_t + B^T P B is diag(2 R0, .) with B[:, 0] = 0, and
+        np.linalg.solve raises on a singular G (trajectory_generation.py:203-204); the kernels divide by 2 R0 and
+        2 R1 + b^T P b.  Q, Q_T >= 0: keeps every P positive semi-definite, so G11 = 2 R1 + b^T P b >= 2 R1 > 0 and
+        1/G11 is in the range the kernels' reciprocal (rcp + two Newton steps, no IEEE range scaling) covers."""
         if not all(np.isfinite(v) and v > 0 for v in self.R):
             raise ValueError(f"R must be positive (G = diag(2 R0, 2 R1 + b^T P b) is inverted), got {self.R}")
+        for name, v in (("Q", self.Q), ("Q_T", self.QT)):
+            if not all(np.isfinite(x) and x >= 0 for x in v):
+                raise ValueError(f"{name} must be non-negative for the gain sweeps (P stays PSD), got {v}")
+        return self
+
+    def c_struct(self) -> _lib.GymWeights:
         w = _lib.GymWeights()
         w.Q[:] = [float(v) for v in self.Q]
         w.R[:] = [float(v) for v in self.R]
@@ -89,8 +98,8 @@ class AcrobotEngine:
         return _lib.stream_handle(self.device)
 
     def set_weights(self, weights: Weights):
-        self.weights = weights
-        self._w = weights.c_struct()
+        w = weights.c_struct()          # first: a failure leaves the engine's weights unchanged
+        self.weights, self._w = weights, w
 
     def pack(self, a: torch.Tensor, Bp: int, W: int = 2) -> torch.Tensor:
         """(B,L,C) lane-major -> SoA (L, C/W, Bp, W): W = 2 pairs (states, gains; wave-blocked, see the ABI header),
@@ -251,8 +260,11 @@ class AcrobotEngine:
                                            J.data_ptr(), B, Bp, N, self.stream), "gym_total_cost")
         return J[:B]
 
-    def backward(self, x, u, x_ref, u_ref, want_lambda=False):
-        """Fused costate + stage lists + Riccati: K (B,T,2,4), sigma (B,T,2), dJ (B,), max|sigma| (B,), lambda."""
+    def backward(self, x, u, x_ref, u_ref, want_lambda=False, check_gains=True):
+        """Fused costate + stage lists + Riccati: K (B,T,2,4), sigma (B,T,2), dJ (B,), max|sigma| (B,), lambda.
+        ``check_gains=False``: the caller uses only lambda (compute_costate_trajectory), which needs no G^-1."""
+        if check_gains:
+            self.weights.require_gain_solvable()
         x = self.t(x); u = self.t(u)
         B, N, _ = x.shape
         T = N - 1

@@ -98,6 +98,7 @@ class BatchedNewtonSolver:
         # the largest shard of the global batch, so that every rank picks the same schedule: the schedules
         # synchronise (all-reduce) at different points, and mixed choices would pair up the wrong collectives.
         sched_B = self.B_sched = int(schedule_lanes) if schedule_lanes is not None else int(B)
+        engine.weights.require_gain_solvable()
         self.eng = engine
         self.x_ref, self.u_ref = engine.refs(x_ref, u_ref, per_lane=True)
         self.B, self.Bp = int(B), padded(int(B))

@@ -130,7 +130,7 @@ def compute_costate_trajectory(x_traj, u_traj, x_ref, u_ref):
     Nn = x_traj.shape[0]
     _, _, _, _, lam = _eng().backward(np.asarray(x_traj, float)[None], np.asarray(u_traj, float)[None][:, :Nn - 1],
                                       np.asarray(x_ref, float)[:Nn], np.asarray(u_ref, float)[:Nn - 1],
-                                      want_lambda=True)
+                                      want_lambda=True, check_gains=False)
     lam = lam[0].cpu().numpy()
     return [lam[t] for t in range(Nn)]
 

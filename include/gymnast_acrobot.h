@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 9
+#define GYM_ABI_VERSION 10
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -144,6 +144,10 @@ typedef struct gym_batch {
 } gym_batch;
 
 int gym_abi_version(void);
+/* Build id: 16 hex digits of the sha256 over the kernel sources and this header the library was compiled from
+ * (gymnast_optimalcontrol_amd/_build.py source_hash).  The Python binding refuses a library whose id differs
+ * from its tree's sources (a stale binary), and the build rebuilds on a mismatch instead of trusting mtimes. */
+const char* gym_build_id(void);
 
 /* [host] Reduce a reference parameter set {m1,m2,l1,lc1,l2,lc2,I1,I2,g,f1,f2} (dynamics.py:15-61). */
 int gym_model_from_params(const double params[11], double dt, gym_model* out);

@@ -30,6 +30,13 @@ def main():
              n_iter=res.n_iter.cpu().numpy(), status=res.status.cpu().numpy(),
              n_rollouts=res.n_rollouts.cpu().numpy(), stats=np.asarray(res.stats_log),
              schedule=np.array(res.schedule))
+    # per-lane references (B_total, N, 4) / (B_total, T, 2): solve_sharded cuts them to the rank's shard
+    xr3 = np.broadcast_to(x_ref, (total,) + x_ref.shape).copy()
+    ur3 = np.broadcast_to(u_ref, (total,) + u_ref.shape).copy()
+    ur3[1::3, :, 1] *= 0.8                       # every third lane follows another reference
+    lo3, hi3, r3 = gd.solve_sharded(x0, xr3, ur3, 40, tol=1e-4, gamma_0=0.1)
+    np.savez(f"{out}.perlane.rank{rank}.npz", lo=lo3, hi=hi3, x=r3.x.cpu().numpy(), cost=r3.cost.cpu().numpy(),
+             n_iter=r3.n_iter.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 

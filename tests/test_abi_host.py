@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "gymnast_acrobot.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(gym_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(gym_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_builds_and_exports_every_declared_symbol():
@@ -29,6 +29,34 @@ def test_library_builds_and_exports_every_declared_symbol():
     out = subprocess_nm(path)
     for name in declared:
         assert name in out, f"{name} not exported by {path}"
+
+
+def test_library_build_id_matches_the_tree():
+    """Stale-binary guard: the library carries the hash of the sources it was compiled from; it equals the tree's
+    (after build(), which rebuilds on any content change), and _lib.load refuses a library whose id differs."""
+    import shutil
+    from gymnast_optimalcontrol_amd import _build, _lib
+    path = _build.build()
+    want = _build.source_hash()
+    assert len(want) == 16 and _build.embedded_build_id(path) == want
+    assert _lib.load(path).gym_build_id().decode() == want
+    assert not _build.needs_build()
+
+
+def test_stale_library_is_refused(tmp_path):
+    """A library whose embedded id is not the tree's (a kernel edited after the build) does not load."""
+    from gymnast_optimalcontrol_amd import _build, _lib
+    path = _build.build()
+    data = open(path, "rb").read()
+    i = data.find(_build.BUILD_ID_TAG) + len(_build.BUILD_ID_TAG)
+    stale = data[:i] + b"0123456789abcdef" + data[i + 16:]
+    if stale == data:
+        stale = data[:i] + b"fedcba9876543210" + data[i + 16:]
+    p = tmp_path / "libstale.so"
+    p.write_bytes(stale)
+    assert _build.embedded_build_id(str(p)) != _build.source_hash()
+    with pytest.raises(ImportError, match="stale binary"):
+        _lib.load(str(p))
 
 
 def subprocess_nm(path):
@@ -154,8 +182,12 @@ def test_weights_from_matrices():
     assert [padded(b) for b in (1, 64, 65, 4096)] == [64, 64, 128, 4096]
     for bad in ((0.0, 1.5), (1e-6, -1.0), (float("nan"), 1.5)):    # singular / invalid G (reference: LinAlgError)
         with pytest.raises(ValueError):
-            Weights(R=bad).c_struct()
-    assert Weights().c_struct().R[1] == 1.5
+            Weights(R=bad).require_gain_solvable()
+        assert Weights(R=bad).c_struct().R[0] == bad[0] or np.isnan(bad[0])   # cost-only paths accept them
+    for badQ in (dict(Q=(1.0, -1.0, 0.0, 0.0)), dict(QT=(1.0, 1.0, float("inf"), 1.0))):
+        with pytest.raises(ValueError):
+            Weights(**badQ).require_gain_solvable()
+    assert Weights().require_gain_solvable().c_struct().R[1] == 1.5
 
 
 def test_product_fails_loudly_without_device():

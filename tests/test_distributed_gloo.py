@@ -207,3 +207,36 @@ def test_gather_sharded_assembles_ragged_shards(tmp_path, world):
     out = str(tmp_path / "g.npy")
     mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     assert np.load(out).all()
+
+
+# ------------------------------------------------------------------ bench.py's own rank launcher
+def _bench(args, env_extra=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["GYM_DIST_BACKEND"] = "gloo"
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=timeout, cwd="/tmp")
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(line[-1]) if line else None), p.stderr
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """bench.py --gpus N with no WORLD_SIZE starts N ranks itself (the driver's 8-GPU run must never silently
+    measure one process): every rank joins one process group (gloo here: no GPU) and rank 0 reports them all."""
+    rc, out, err = _bench(["--gpus", "3", "--dry-run"])
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 3 and out["dist"] == {"backend": "gloo", "world_size": 3,
+                                                  "launcher": "bench.py (spawned ranks)"}
+    assert out["ranks"] == [0, 1, 2] and len(set(out["pids"])) == 3
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    """Under a launcher, WORLD_SIZE must equal --gpus: exit status 2, nothing printed on stdout."""
+    rc, out, err = _bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and out is None and "WORLD_SIZE=1" in err
+    rc, out, _ = _bench(["--gpus", "1", "--dry-run"])
+    assert rc == 0 and out["n_gpus"] == 1 and out["dist"]["world_size"] == 1 and out["dist"]["backend"] is None

@@ -238,4 +238,64 @@ def test_sharded_solve_on_hip_matches_unsharded(total, tmp_path):
         for k, v in full.items():
             assert np.array_equal(p_[k], v[lo:hi], equal_nan=True), (k, lo, hi)
     assert (full["n_rollouts"] > full["n_iter"]).any()        # some lanes backtracked
+    # per-lane references cut to each rank's shard (sharded_worker.py): bit for bit the unsharded per-lane solve
+    xr3 = np.broadcast_to(x_ref, (total,) + x_ref.shape).copy()
+    ur3 = np.broadcast_to(u_ref, (total,) + u_ref.shape).copy()
+    ur3[1::3, :, 1] *= 0.8
+    r3 = BatchedNewtonSolver(AcrobotEngine(), xr3, ur3, total, tol=1e-4, gamma_0=0.1).solve(x0, 40)
+    for rk in range(2):
+        p3 = np.load(f"{out}.perlane.rank{rk}.npz")
+        lo, hi = int(p3["lo"]), int(p3["hi"])
+        for k in ("x", "cost", "n_iter"):
+            assert np.array_equal(p3[k], getattr(r3, k)[lo:hi].cpu().numpy(), equal_nan=True), (k, rk)
     torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------ the RCCL branch on one GPU
+def test_rccl_collectives_on_one_gpu(tmp_path):
+    """The device-tensor RCCL branches of distributed.py, executed before the driver's 8-GPU run does: a 1-rank
+    group on backend "nccl" (with device_id), solve_sharded(gather=True, force_collectives=True) on the
+    persistent, pipelined and serial schedules, max_over_ranks / sum_over_ranks, and per-lane references cut to
+    the shard.  Every all-reduce is on a fp64 device tensor enqueued from the solver's stream, every result field
+    is all-gathered on the device, and the gathered results are bit for bit the plain solve's (tests/rccl_worker.py
+    checks; it runs in its own process so the process group cannot leak into other tests)."""
+    import json
+    out = tmp_path / "rccl.json"
+    env = dict(os.environ)
+    env.pop("GYM_DIST_BACKEND", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py"), str(out), "301", "600"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    s = json.loads(out.read_text())
+    assert s["backend"] == "nccl" and s["world_size"] == 1
+    assert set(s["schedules"]) == {"persistent", "pipelined", "serial"}
+    for sched, d in s["schedules"].items():
+        assert d["all_reduce_calls"] >= 1 and d["all_gather_calls"] == 9, (sched, d)
+        assert d["backtracked"] > 0                      # the wide-start lanes exercise the retry path too
+
+
+# ------------------------------------------------------------------ bench.py --gpus N without a launcher
+def test_bench_spawns_ranks_on_the_gpu():
+    """bench.py --gpus 2 with no launcher starts two ranks itself (gloo: both share this GPU; RCCL refuses two
+    ranks on one device): the line reports n_gpus 2, a 2-rank process group and twice the lanes; rank 0's shard
+    is the N = 1 workload, so lane 0's parity record and the per-GPU lane count equal the single-process line's."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["GYM_DIST_BACKEND"] = "gloo"
+    args = ["--batch", "512", "--steps", "1", "--warmup", "0", "--no-cpu", "--extra-legs", ""]
+
+    def line(n):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *args], env=env,
+                           capture_output=True, text=True, timeout=280)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+    two, one = line(2), line(1)
+    assert two["n_gpus"] == 2 and two["dist"]["world_size"] == 2 and two["dist"]["backend"] == "gloo"
+    assert two["dist"]["launcher"] == "bench.py (spawned ranks)"
+    assert one["n_gpus"] == 1 and one["dist"]["world_size"] == 1
+    assert two["config"]["global_lanes"] == 1024 and two["config"]["lanes_per_gpu"] == 512
+    assert one["config"]["global_lanes"] == one["config"]["lanes_per_gpu"] == 512
+    for k in ("lane0_iters", "lane0_rel_l2_x", "lane_iters_min_max"):
+        assert two["parity"][k] == one["parity"][k], k
+    assert two["value"] > 0 and two["scaling"] == "weak"

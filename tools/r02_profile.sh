@@ -7,15 +7,15 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r02
 mkdir -p $OUT
 fault() { grep -q -i -E "illegal memory access|memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "$1"; }
-run() {  # run <name> <seconds> <cmd...>
+run() {  # run <name> <seconds> <cmd...>   (status 1 is tolerated for the pytest step only)
   local name=$1 secs=$2; shift 2
   echo "[$(date +%T)] start $name" | tee -a $OUT/steps.log
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "[$(date +%T)] end $name rc=$rc" | tee -a $OUT/steps.log
   tail -2 "$OUT/$name.log" | cut -c1-300
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
   if fault "$OUT/$name.log"; then echo "GPU fault in $name: stopping"; exit 3; fi
+  if [ $rc -ne 0 ] && ! { [ $rc -eq 1 ] && [ "$name" = pytest_gpu ]; }; then echo "stopping after $name"; exit $rc; fi
 }
 for s in "$@"; do
   case $s in
