@@ -3,7 +3,10 @@
 Names, argument meaning and return conventions follow /root/reference/dynamics.py:
   dt, ns, ni (:173-175); dynamics(xx, uu) (:177-195, RK4); continuous_dynamics(xx, uu)
   (:197-213); Calculate_A_B_matrixes(x_t, u_t) -> (A_c, B_c) (:217-226); params_1/2/3 (:15-61);
-  set_params(version_num) (:117-144).
+  set_params(version_num) (:117-144), returning sympy matrices as the reference does; the symbolic layer
+  (theta1, theta2, ..., M, C, Gvec, F, M_func, RHS_func, f_cont_sym, A_sym, B_sym, func_A, func_B, ...; :5-170)
+  is built with sympy on first access (module __getattr__; ``from dynamics import *`` builds it, as importing
+  the reference does).
 Inputs are numpy arrays (as in the reference); the arithmetic runs in gfx950 kernels
 (gym_rk4_step / gym_continuous_dynamics / gym_jacobians) and results come back as numpy.
 Extensions: every function also accepts a stack of points (n,4)/(n,2) and returns (n,...);
@@ -49,6 +52,14 @@ def use_params(version_num: int = 1):
 
 
 def set_params(version_num):
+    """(M, C, G, F) of a parameter set as sympy matrices in theta1, theta2, theta1_dot, theta2_dot
+    (dynamics.py:117-144), as the reference returns them (its compute_equilibrium lambdifies G over theta1,
+    theta2); needs sympy.  set_params_numeric is the sympy-free numeric form."""
+    from ._symbolic import set_params as sym
+    return sym(version_num)
+
+
+def set_params_numeric(version_num):
     """Numeric (M, C, G, F) of a parameter set (dynamics.py:117-144); no side effects.
 
     Returns callables M(th1, th2) (2,2), C(th1, th2, w1, w2) (2,2), G(th1, th2) (2,), and F (2,2),
@@ -105,3 +116,27 @@ def Calculate_A_B_matrixes(x_t, u_t):
     A, B = engine().jacobians(x, u)
     A, B = A.cpu().numpy(), B.cpu().numpy()
     return (A[0], B[0]) if single else (A, B)
+
+
+_SYMBOLIC = None
+
+
+def __getattr__(name):
+    """The reference's symbolic names (dynamics.py:5-170), built with sympy on first access."""
+    global _SYMBOLIC
+    from ._symbolic import NAMES
+    if name not in NAMES:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    if _SYMBOLIC is None:
+        from ._symbolic import model
+        _SYMBOLIC = model()
+    return _SYMBOLIC[name]
+
+
+def _public():
+    from ._symbolic import NAMES
+    return ["dt", "ns", "ni", "params_1", "params_2", "params_3", "set_params", "dynamics", "continuous_dynamics",
+            "Calculate_A_B_matrixes", *NAMES]
+
+
+__all__ = _public()

@@ -60,6 +60,7 @@ class SolveResult:
     hist_smax: torch.Tensor | None = None   # (hist_len, B)
     x_trajs: dict | None = None             # {lane: [x_0, x_1, ...]} of the captured lanes (capture_lanes)
     cost0: dict | None = None               # {lane: J_0} of the captured lanes
+    sigmas: dict | None = None              # {lane: {iteration: sigma (T,2)}} of the captured lanes (capture_sigma)
     schedule: str = ""                      # "serial" | "pipelined" | "persistent"
 
 
@@ -91,7 +92,8 @@ class BatchedNewtonSolver:
                  max_ls: int = MAX_LINE_SEARCH_ITERS, hist_len: int = 0, pipeline: bool | None = None,
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
-                 capture_lanes=None, capture_every: int = 1, split_waves: bool = True):
+                 capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
+                 capture_sigma=(0, 1, 2)):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -196,8 +198,12 @@ class BatchedNewtonSolver:
             if any(not (0 <= i < self.B) for i in self.capture_lanes):
                 raise ValueError(f"capture_lanes must lie in [0, {self.B})")
         self.capture_every = max(int(capture_every), 1)
+        # sigma of the captured lanes at these iterations (the reference's report plots iterations 0, 1, 2 and the
+        # last, trajectory_generation.py:341, 476-480; the last one is the solve's own sigma output)
+        self.capture_sigma = tuple(sorted({int(i) for i in (capture_sigma or ())}))
         self._cap_pos = None
         self._cap_log = []
+        self._sig_log = []
 
     @property
     def schedule(self) -> str:
@@ -286,6 +292,7 @@ class BatchedNewtonSolver:
     def _capture_start(self, positions):
         """Begin capturing the lanes at internal positions ``positions`` (after init: the open-loop rollout)."""
         self._cap_log = []
+        self._sig_log = []
         if self.capture_lanes is None:
             self._cap_pos = None
             return
@@ -307,6 +314,11 @@ class BatchedNewtonSolver:
         x = xb.view(self.N, W, 2, 64, 2)[:, pos // 64, :, pos % 64, :].reshape(-1, self.N, 4)
         self._cap_log.append((self.k, x.clone(), self.n_iter[pos].clone(), self.status[pos].clone(),
                               self.cost[pos].clone()))
+        if not initial and (self.k - 1) in self.capture_sigma:
+            # iteration k-1's sigma: gym_newton_sigma re-runs each lane's sweep at the iterate of its last
+            # iteration (the same bits as that iteration's own sweep); it writes only the sigma1 plane, which every
+            # schedule rewrites before reading it, so the solve is unchanged
+            self._sig_log.append((self.k - 1, self.sigma()[pos].clone(), self.n_iter[pos].clone()))
 
     def captured_trajectories(self) -> dict:
         """{caller lane: [x_0, x after each accepted iteration ...]} as (N,4) numpy arrays -- the reference's
@@ -321,6 +333,19 @@ class BatchedNewtonSolver:
                     out[lane].append(x[j])
                 elif n_it[j] == k and st[j] != _lib.LS_FAILED:   # the lane ran iteration k-1 and accepted it
                     out[lane].append(x[j])
+        return out
+
+    def captured_sigmas(self) -> dict:
+        """{caller lane: {iteration i: sigma (T,2)}} for the iterations of ``capture_sigma`` each captured lane ran
+        (the reference's history['sigmas'][i])."""
+        if self.capture_lanes is None:
+            return {}
+        out = {lane: {} for lane in self.capture_lanes}
+        for it, sg, n_it in self._sig_log:
+            sg, n_it = sg.cpu().numpy(), n_it.cpu().numpy()
+            for j, lane in enumerate(self.capture_lanes):
+                if n_it[j] == it + 1:                    # the lane ran iteration it
+                    out[lane][it] = sg[j]
         return out
 
     def captured_initial_costs(self) -> dict:
@@ -432,6 +457,7 @@ class BatchedNewtonSolver:
         iters = int(n_iter.max().item()) if self.persistent else self.k
         res["x_trajs"] = self.captured_trajectories() if self.capture_lanes is not None else None
         res["cost0"] = self.captured_initial_costs() if self.capture_lanes is not None else None
+        res["sigmas"] = self.captured_sigmas() if self.capture_lanes is not None else None
         res["schedule"] = self.schedule
         return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
                            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)

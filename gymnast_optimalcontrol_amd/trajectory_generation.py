@@ -29,7 +29,7 @@ import torch
 
 from . import _lib
 from .dynamics import (Calculate_A_B_matrixes, continuous_dynamics, dt, dynamics, engine, ni, ns,  # noqa: F401
-                       set_params, use_params)
+                       set_params, set_params_numeric, use_params)
 from .engine import Weights
 from .params import MAX_LINE_SEARCH_ITERS
 from .solver import BatchedNewtonSolver, SolveResult, newton_solve_batch  # noqa: F401
@@ -54,7 +54,7 @@ def _eng():
 def compute_equilibrium(u_target, theta_guess):
     """Solve G(theta1, theta2) = u_target (:22-39) with scipy's hybrid root finder."""
     from scipy.optimize import root
-    _, _, G, _ = set_params(1)
+    _, _, G, _ = set_params_numeric(1)          # the numbers of set_params(1)'s G, without sympy
     u_target = np.asarray(u_target, dtype=float)
     sol = root(lambda th: np.asarray(G(th[0], th[1]), dtype=float).reshape(-1) - u_target, theta_guess,
                method="hybr")
@@ -271,7 +271,10 @@ def generate_report_graphs(t_ref, x_ref, u_ref, x_opt, u_opt, history):
     u_ref = np.asarray(u_ref, float)
     u_ref = u_ref[:-1] if u_ref.shape[0] == t_ref.shape[0] else u_ref
     shown = report_iterations(len(history["x_trajs"]))
-    sig_its = sorted({i for i in (0, 1, 2, len(history["sigmas"]) - 1) if 0 <= i < len(history["sigmas"])})
+    # the reference's selection (:476-477); a batched lane's history holds sigma only at the iterations it
+    # recorded (None elsewhere)
+    sig_its = sorted({i for i in (0, 1, 2, len(history["sigmas"]) - 1)
+                      if 0 <= i < len(history["sigmas"]) and history["sigmas"][i] is not None})
     data = {"iterations_shown": shown, "sigma_iterations": sig_its,
             "sigma_tau2": {i: np.asarray(history["sigmas"][i], float).reshape(-1, 2)[:, 1] for i in sig_its},
             "cost": np.asarray(history["cost"], float), "sigma_norm": np.asarray(history["sigma_norm"], float)}
@@ -408,14 +411,21 @@ def newton_Algorithm_batch(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.
 
 def lane_history(res: SolveResult, lane: int) -> dict:
     """The reference's ``history`` dict (:321-327) of one lane of a batched solve, for generate_report_graphs:
-    cost and sigma_norm from the per-lane histories (hist_len), x_trajs from capture_lanes.  'sigmas' holds the
-    lane's last-iteration sigma only (the batched solver does not keep every iteration's sigma)."""
+    cost and sigma_norm from the per-lane histories (hist_len), x_trajs from capture_lanes.  'sigmas' has the
+    reference's length (one entry per iteration the lane ran, :341) and holds sigma (T,2) at the iterations the
+    report plots -- the solver's capture_sigma iterations (0, 1, 2 by default) and the last one (the solve's sigma
+    output) -- and None at the others (the batched solver does not keep every iteration's sigma)."""
     if res.hist_cost is None or res.x_trajs is None or lane not in res.x_trajs:
         raise ValueError("lane_history needs a solve with hist_len > 0 and the lane in capture_lanes")
     n = int(res.n_iter[lane])
     failed = int(res.status[lane]) == _lib.LS_FAILED
     hc = res.hist_cost[:, lane].cpu().numpy()
     hs = res.hist_smax[:, lane].cpu().numpy()
+    sigmas = [None] * n
+    for it, sg in (res.sigmas or {}).get(lane, {}).items():
+        if it < n:
+            sigmas[it] = np.asarray(sg)
+    if n:
+        sigmas[n - 1] = res.sigma[lane].cpu().numpy()
     return {"cost": [res.cost0[lane]] + [float(v) for v in hc[:n - 1 if failed else n]],
-            "sigma_norm": [float(v) for v in hs[:n]], "x_trajs": res.x_trajs[lane],
-            "sigmas": [res.sigma[lane].cpu().numpy()]}
+            "sigma_norm": [float(v) for v in hs[:n]], "x_trajs": res.x_trajs[lane], "sigmas": sigmas}

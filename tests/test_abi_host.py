@@ -225,6 +225,44 @@ def test_reference_surface_names_exist():
               "newton_Algorithm", "get_fully_actuated_ref"):
         assert hasattr(tg, n), n
     assert tg.N == 501 and d.dt == 0.02 and tg.nx == 4 and tg.nu == 2
+    for n in ("generate_report_graphs", "plot_results", "lane_history", "newton_Algorithm_batch"):
+        assert hasattr(tg, n), n
+
+
+def test_symbolic_dynamics_surface_matches_reference(golden):
+    """The reference's symbolic layer (dynamics.py:5-170; sympy, built on first access) against the reference-run
+    KATs: f_cont_sym / A_sym / B_sym lambdified (calc_continuous_dynamics, func_A, func_B) at the 64 KAT points,
+    M_func / RHS_func (the fully actuated form with tau1 = 0), and the reference's own compute_equilibrium recipe
+    -- lambdify(set_params(1)[2]) over (theta1, theta2) -- on the task-1 golden equilibria; every name of the
+    reference's module-level surface comes with ``from dynamics import *``."""
+    pytest.importorskip("sympy")
+    import sympy as sp
+    from scipy.optimize import root
+    from gymnast_optimalcontrol_amd import dynamics as d
+    g = golden("kat_primitives")
+    X, U = g["X"], g["U"]
+    for i in range(0, 64, 7):
+        args = [*X[i], *U[i]]
+        np.testing.assert_allclose(np.array(d.calc_continuous_dynamics(*args), float).ravel(), g["f_cont"][i],
+                                   rtol=1e-11, atol=1e-11)
+        np.testing.assert_allclose(np.array(d.func_A(*args), float), g["A_c"][i], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(np.array(d.func_B(*args), float), g["B_c"][i], rtol=1e-10, atol=1e-12)
+        qdd = np.linalg.solve(d.M_func(*X[i, :2]), np.asarray(d.RHS_func(*X[i], 0.0, U[i, 1]), float).ravel())
+        np.testing.assert_allclose(qdd, g["f_cont"][i, 2:], rtol=1e-11, atol=1e-11)
+    G_func = sp.lambdify((d.theta1, d.theta2), d.set_params(1)[2], "numpy")     # trajectory_generation.py:25-26
+    t1 = golden("task1_solve")
+    for x_e, u_t, guess in ((t1["x_e1"], (0.0, 0.0), (0.1, -0.1)), (t1["x_e2"], (0.5, 0.5), (0.35, -0.35))):
+        sol = root(lambda th: np.array(G_func(th[0], th[1]), float).reshape(-1) - np.asarray(u_t), guess,
+                   method="hybr")
+        np.testing.assert_allclose(sol.x, x_e[:2], atol=1e-10)
+    assert [type(m).__name__ for m in d.set_params(3)] == ["MutableDenseMatrix"] * 4
+    ns = {}
+    exec("from gymnast_optimalcontrol_amd.dynamics import *", ns)
+    for n in ("theta1", "theta2", "M_func", "RHS_func", "f_cont_sym", "A_sym", "B_sym", "func_A", "func_B",
+              "M", "C", "Gvec", "F", "set_params", "dynamics", "dt", "params_1"):
+        assert n in ns, n
+    with pytest.raises(AttributeError):
+        d.not_a_reference_name
 
 
 def test_host_setup_functions_match_reference(golden):

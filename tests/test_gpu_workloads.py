@@ -174,6 +174,11 @@ def test_capture_lanes_reproduce_reference_history(schedule, task2_refs):
                             hist_len=1000, pipeline=schedule == "pipelined", persistent=schedule == "persistent")
     r = s.solve(x0, 5000)
     assert r.schedule == schedule
+    # capturing (trajectories, and sigma re-runs at iterations 0-2) leaves the solve bit for bit unchanged
+    r_plain = BatchedNewtonSolver(AcrobotEngine(), xr, ur, 70, tol=1e-4, gamma_0=0.1, hist_len=1000,
+                                  pipeline=schedule == "pipelined", persistent=schedule == "persistent").solve(x0, 5000)
+    for k in ("x", "u", "K", "sigma", "cost", "n_iter", "n_rollouts", "status"):
+        assert np.array_equal(getattr(r, k).cpu().numpy(), getattr(r_plain, k).cpu().numpy(), equal_nan=True), k
     tr = r.x_trajs
     assert len(tr[0]) == len(g["cost_hist"]) == 394
     for j, it in enumerate(g["x_hist_idx"]):     # x_0 of the golden lane is the rest state: all zeros
@@ -190,8 +195,18 @@ def test_capture_lanes_reproduce_reference_history(schedule, task2_refs):
     h = tg.lane_history(r, 0)
     np.testing.assert_allclose(h["cost"], g["cost_hist"], rtol=1e-9)
     np.testing.assert_allclose(h["sigma_norm"], g["sigma_norm_hist"], rtol=1e-6)
+    # history['sigmas'] (:341): the reference's length, sigma at the iterations its report plots (:476-480)
+    assert len(h["sigmas"]) == 393 and sorted(r.sigmas[0]) == [0, 1, 2]
+    assert rel_l2(h["sigmas"][0], g["sigma_first"]) < 1e-8
+    assert rel_l2(h["sigmas"][392], g["sigma"]) < 1e-6
+    assert all(h["sigmas"][i] is None for i in range(3, 392))
+    # the lane that fails the line search: sigma of its iterations 0-2 and of its last (failed) iteration
+    hf = tg.lane_history(r, 33)
+    assert len(hf["sigmas"]) == int(r.n_iter[33]) and sorted(r.sigmas[33]) == [0, 1, 2]
     d = tg.generate_report_graphs(g["t_ref"], g["x_ref"], g["u_ref"], r.x[0].cpu().numpy(), r.u[0].cpu().numpy(), h)
     assert d["iterations_shown"][-1] == 393 and len(d["figures"]) == 4
+    assert d["sigma_iterations"] == [0, 1, 2, 392]
+    np.testing.assert_array_equal(d["sigma_tau2"][392], r.sigma[0, :, 1].cpu().numpy())
     import matplotlib.pyplot as plt
     plt.close("all")
 
