@@ -56,7 +56,7 @@ def main():
     assert dist.is_initialized() and dist.get_backend() == "nccl" and dist.get_world_size() == 1, dist.get_backend()
     torch.cuda.set_device(gd.local_device_index(local_rank))
     x_ref, u_ref = load_refs()
-    x0 = sharded_x0(total, 11)
+    x0 = sharded_x0(total, 7)           # seed 7: backtracking lanes at 301 lanes (test_sharded_solve_on_hip...)
     eng = AcrobotEngine()
     summary = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "schedules": {}}
     kw = dict(tol=1e-4, gamma_0=0.1)
