@@ -2168,6 +2168,232 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Straggler tail (gym_newton_tail).  Late in a hard solve a handful of lanes keep iterating for thousands of
+// outer iterations, many of them backtracking (SURVEY 8(d)'s stress variant: one lane to 5,000 iterations, the
+// last ~4,000 serving a few lanes).  The lock-step schedules then pay, per iteration and lane, one sweep chain
+// and one trial chain on one thread each, plus for a backtracking lane the sigma1 re-run, the candidate pass and
+// the accepted candidate's re-run.  Here one workgroup (one wavefront) owns one listed lane and runs its own
+// iterations k0 .. k1-1 back to back (lanes are independent problems; the persistent schedule's argument):
+//   sweep  : the 64 threads evaluate the Jacobians / linearisations of 64 stages at once (stage_lin, a function
+//            of x_t, u_t only) into LDS, then run the Riccati recursion (step_lin) over those stages, reading
+//            them back; K row 1, cg and sigma1 are stored in the same pass (no sigma1 re-run);
+//   trials : thread c evaluates Armijo trial c (gamma_0 beta^c, formed sequentially as the reference does) --
+//            all max_ls of them at once, each writing its candidate into a scratch slot -- and the first
+//            accepted one (ballot) is copied into the lane's next state buffer.
+// Every value is the one the serial schedule computes (the same device functions: jacobian, stage_lin, step_lin,
+// store_stage, trial_u0 / trial_u1, stage_cost, rk4): trial 1 is the offset form cg + K1 x_new, trial c > 0
+// fma(gamma_c - gamma_0, sigma1, cg + K1 x_new), so decisions, rollout counts and trajectories are the same bits.
+// ------------------------------------------------------------------------------------------
+constexpr int TL_STAGES = BLK;   // stages per linearisation pass (one per thread)
+constexpr int TL_PITCH = 22;     // doubles per stage in LDS: Lin (16), x_t (4), u1_t; padded to an even count
+struct TailArgs {
+    Dyn m;
+    KW w;
+    SolverCtl a;
+    double2* x[2];
+    double* u[2];
+    double2* K1;
+    double* cs;
+    const double* xr;
+    const double* ur;
+    double *cost, *dJ, *smax, *gamma;
+    int32_t *status, *n_iter, *res_buf, *n_roll;
+    double *hist_cost, *hist_smax;
+    const int32_t* list;   // the lanes, one workgroup each
+    double2* sx;           // candidate scratch: x (N, Vp/64, 2, 64) double2 over virtual lanes (slot * max_ls + c)
+    double* su;            // ... and u planes (T, 2, Vp)
+    int64_t Bp, Vp;
+    int32_t N, k0, k1, pad;
+};
+static_assert(offsetof(TailArgs, w) == 96, "kernarg layout: KW at byte 96 (kernarg_consts)");
+typedef const TailArgs* targs_t;
+__device__ __forceinline__ targs_t tail_args() {
+    const __attribute__((address_space(4))) TailArgs* p =
+        (const __attribute__((address_space(4))) TailArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (targs_t)p;
+}
+
+// the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage; returns dJ, max|sigma|
+template <bool U0Z, bool RL>
+__device__ __forceinline__ void tail_sweep(double* lin, int lane, int64_t l, int cb, double& dJ_out,
+                                           double& smax_out) {
+    const targs_t R = tail_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double2* x = R->x[cb];
+    const double* u = R->u[cb];
+    const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+    const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double g0 = R->a.gamma0;
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
+    for (int tb = T - 1; tb >= 0; tb -= TL_STAGES) {
+        const int t = tb - lane;   // this thread's stage of the pass
+        if (t >= 0) {
+            const double2 xa = x[wix(t, 0, 2, l, Bp)], xb = x[wix(t, 1, 2, l, Bp)];
+            const double u0 = U0Z ? 0.0 : u[pix(t, 0, 2, l, Bp)], u1 = u[pix(t, 1, 2, l, Bp)];
+            const KArgs ka = kernarg_consts();
+            const gym::Jac J = gym::jacobian(ka.m, xa.x, xa.y, xb.x, xb.y, u1);
+            const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, xa, xb, u0, u1, xr + 4 * t, ur + 2 * t);
+            double* s = lin + lane * TL_PITCH;
+            s[0] = L.A20; s[1] = L.A21; s[2] = L.A22; s[3] = L.A23;
+            s[4] = L.A30; s[5] = L.A31; s[6] = L.A32; s[7] = L.A33;
+            s[8] = L.bd2; s[9] = L.bd3; s[10] = L.q0; s[11] = L.q1;
+            s[12] = L.q2; s[13] = L.q3; s[14] = L.r0; s[15] = L.r1;
+            s[16] = xa.x; s[17] = xa.y; s[18] = xb.x; s[19] = xb.y; s[20] = u1;
+        }
+        __syncthreads();
+        const int n = tb + 1 < TL_STAGES ? tb + 1 : TL_STAGES;
+        for (int i = 0; i < n; ++i) {   // every thread runs the recursion (the same bits); thread 0 stores
+            const double* s = lin + i * TL_PITCH;
+            const KArgs ka = kernarg_consts();
+            const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                        s[10], s[11], s[12], s[13], s[14], s[15], ka.m.h};
+            double k0, k1, k2, k3, s0, s1;
+            S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
+            if (lane == 0)
+                store_stage<OUT_ALL>(Kb, Cb, tb - i, row, plane, o2, o1, make_double2(s[16], s[17]),
+                                     make_double2(s[18], s[19]), s[20], g0, k0, k1, k2, k3, s1);
+        }
+        __syncthreads();
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) into virtual lane v of the
+// scratch; returns the candidate's cost
+template <bool U0Z, bool RL>
+__device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, double g, int64_t v) {
+    const targs_t R = tail_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+    const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const uint32_t v2 = wbo(v, 2), v1o = (uint32_t)v * 8u;
+    const uint32_t srow = (uint32_t)R->Vp * 16u, splane = (uint32_t)R->Vp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
+    const char* Xs = reinterpret_cast<const char*>(R->sx);
+    const char* Us = reinterpret_cast<const char*>(R->su);
+    const double gamma0 = R->a.gamma0, dg = g - gamma0;
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    {
+        const auto rX = rsrc(Xs);
+        bst2(rX, v2, 0, n0, n1);
+        bst2(rX, v2, WROW, n2, n3);
+    }
+    double J = 0.0;
+    auto fetch = [&](TrialStage& q, int t) {
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        q.k0 = bld2<0>(rK, o2, 0);
+        q.k1 = bld2<0>(rK, o2, WROW);
+        const auto rC = rsrc(Cb + (int64_t)t * row);
+        q.cg = bld1<0>(rC, o1, 0);
+        q.s1 = bld1<0>(rC, o1, plane);
+        q.u0 = U0Z ? 0.0 : bld1<0>(rsrc(Ub + (int64_t)t * row), o1, 0);
+    };
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    TrialStage pre;
+    fetch(pre, 0);
+    for (int t = 0; t < T; ++t) {
+        const TrialStage q = pre;
+        if (t + 1 < T) fetch(pre, t + 1);
+        const double* urt = ur + 2 * t;
+        const KArgs ka = kernarg_consts();
+        const double v0 = U0Z ? 0.0 : trial_u0(q.u0, urt[0], g, ka.w.G00, ka.w.iG00);
+        const double y = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
+        const double ysig = __builtin_fma(dg, q.s1, y);                 // trial_u1_sig's value
+        const double u1 = c == 0 ? y : ysig;
+        const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = u1 - urt[1];
+        J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
+        const auto rO = rsrc(Us + (int64_t)t * srow);
+        if (!U0Z) bst1(rO, v1o, 0, v0);
+        bst1(rO, v1o, splane, u1);
+        gym::rk4(ka.m, n0, n1, n2, n3, u1, pk);
+        const auto rX = rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow));
+        bst2(rX, v2, 0, n0, n1);
+        bst2(rX, v2, WROW, n2, n3);
+    }
+    const KArgs ka = kernarg_consts();
+    return J + xcost(ka.w.QT, n0, n1, n2, n3, xr + 4 * T);
+}
+
+template <bool U0Z, bool RL>
+__global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
+    __shared__ double lin[TL_STAGES * TL_PITCH];
+    const int lane = threadIdx.x;
+    const int64_t l = tail_args()->list[blockIdx.x];
+    int st = tail_args()->status[l];
+    for (int k = tail_args()->k0; st == GYM_ACTIVE && k < tail_args()->k1; ++k) {
+        const int cb = k & 1;
+        double dJ, sm;
+        tail_sweep<U0Z, RL>(lin, lane, l, cb, dJ, sm);
+        {
+            const targs_t Q = tail_args();
+            if (lane == 0) {
+                Q->dJ[l] = dJ;
+                Q->smax[l] = sm;
+                if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = sm;
+            }
+        }
+        lane_fence();   // K1 / cg / sigma1 of this sweep visible to every thread's loads
+        const int max_ls = tail_args()->a.max_ls;
+        const int64_t v = (int64_t)blockIdx.x * max_ls + lane;
+        double g = tail_args()->a.gamma0;
+        for (int q = 0; q < lane && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
+        bool ok = false;
+        double Jn = 0.0;
+        if (lane < max_ls) {
+            Jn = tail_candidate<U0Z, RL>(l, cb, lane, g, v);
+            const targs_t R = tail_args();
+            ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
+        }
+        const unsigned long long acc = __ballot(ok);
+        const int first = acc ? __ffsll((long long)acc) - 1 : -1;   // the first accepted trial, in order
+        const int nr = first >= 0 ? first + 1 : max_ls;
+        lane_fence();   // the candidates' scratch stores, before the copy reads them
+        if (first >= 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
+            const targs_t R = tail_args();
+            const int T = R->N - 1;
+            const int64_t vf = (int64_t)blockIdx.x * max_ls + first;
+            for (int t = lane; t <= T; t += BLK) {
+                R->x[cb ^ 1][wix(t, 0, 2, l, R->Bp)] = R->sx[wix(t, 0, 2, vf, R->Vp)];
+                R->x[cb ^ 1][wix(t, 1, 2, l, R->Bp)] = R->sx[wix(t, 1, 2, vf, R->Vp)];
+                if (t < T) {
+                    if (!U0Z) R->u[cb ^ 1][pix(t, 0, 2, l, R->Bp)] = R->su[pix(t, 0, 2, vf, R->Vp)];
+                    R->u[cb ^ 1][pix(t, 1, 2, l, R->Bp)] = R->su[pix(t, 1, 2, vf, R->Vp)];
+                }
+            }
+        }
+        const double Jf = __shfl(Jn, first >= 0 ? first : 0);
+        const double gf = __shfl(g, first >= 0 ? first : 0);
+        if (lane == 0) {
+            const targs_t F = tail_args();
+            F->n_roll[l] += nr;
+            F->n_iter[l] += 1;
+            SolverCtl c = F->a;
+            c.k = k;
+            if (first >= 0)
+                accept_lane(c, l, Jf, gf, sm, F->cost, F->gamma, F->status, F->res_buf, F->hist_cost, F->Bp);
+            else
+                fail_lane(c, l, F->status, F->res_buf);
+        }
+        st = first < 0 ? GYM_LS_FAILED : (sm < tail_args()->a.tol ? GYM_CONVERGED : GYM_ACTIVE);
+        lane_fence();   // the next iterate and the lane's state visible to the next iteration
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Armijo gamma sweeps (plot_armijo_line_search :254-265): J(gamma_g) of the candidate rollout for G step
 // sizes per lane, cost only, one thread per (lane, g).  The G blocks of one lane group re-read the same
 // streams, so a group's blocks are mapped onto one XCD (blocks are dealt round-robin over the 8 XCDs) and
@@ -2723,6 +2949,51 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
     }
     // the statistics after iteration k1 - 1 ("lanes that ran" = the lanes that executed it; [4] = 0: this
     // schedule keeps no retry list)
+    hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
+                       b->n_iter, b->n_roll, b->partials, Range{0, b->B}, (int)k1 - 1);
+    hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64 * NSTAT), 0, st, b->partials, b->counters, b->stats,
+                       (const double*)nullptr, (double*)nullptr, STAT_BLOCKS);
+    return launch_status();
+}
+
+int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t* doubles_out) {
+    if (!doubles_out || N < 2 || n_lanes < 0 || max_ls < 1 || max_ls > BLK) return GYM_EINVAL;
+    const int64_t v = (int64_t)n_lanes * max_ls;
+    const int64_t Vp = v > 0 ? (v + BLK - 1) / BLK * BLK : BLK;
+    *doubles_out = Vp * (4 * (int64_t)N + 2 * (int64_t)(N - 1));
+    return 0;
+}
+
+int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
+                    const int32_t* lanes, int32_t n_lanes, double* scratch, int64_t scratch_doubles, int32_t k0,
+                    int32_t k1, void* s) {
+    int64_t need = 0;
+    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || n_lanes < 0 || (n_lanes > 0 && (!lanes || !scratch)) ||
+        (b->flags & GYM_FLAG_X_CKPT) || gym_newton_tail_scratch(b->N, n_lanes, a->max_ls, &need) ||
+        scratch_doubles < need || (int64_t)n_lanes > b->B)
+        return GYM_EINVAL;
+    hipStream_t st = (hipStream_t)s;
+    const bool hist = a->record_history != 0;
+    if (k1 > k0 && n_lanes > 0) {
+        TimedLaunch tl(b->timing, 9, st);
+        TailArgs ta;
+        ta.m = Dyn(*m);
+        ta.w = kw(*w);
+        ta.a = SolverCtl{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k0, b->hist_len, 0};
+        for (int i = 0; i < 2; ++i) { ta.x[i] = (double2*)b->x[i]; ta.u[i] = b->u[i]; }
+        ta.K1 = (double2*)b->K1; ta.cs = b->cs; ta.xr = b->x_ref; ta.ur = b->u_ref;
+        ta.cost = b->cost; ta.dJ = b->dJ; ta.smax = b->smax; ta.gamma = b->gamma;
+        ta.status = b->status; ta.n_iter = b->n_iter; ta.res_buf = b->res_buf; ta.n_roll = b->n_roll;
+        ta.hist_cost = hist ? b->hist_cost : nullptr; ta.hist_smax = hist ? b->hist_smax : nullptr;
+        ta.list = lanes;
+        const int64_t v = (int64_t)n_lanes * a->max_ls;
+        ta.Vp = (v + BLK - 1) / BLK * BLK;
+        ta.sx = (double2*)scratch;
+        ta.su = scratch + 4 * (int64_t)b->N * ta.Vp;
+        ta.Bp = b->Bp; ta.N = b->N; ta.k0 = k0; ta.k1 = k1; ta.pad = 0;
+        hipLaunchKernelGGL(RUN_SEL(b, k_nt_tail), dim3((unsigned)n_lanes), dim3(BLK), 0, st, ta);
+    }
+    // the statistics after iteration k1 - 1, over the whole batch (as gym_newton_run)
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
                        b->n_iter, b->n_roll, b->partials, Range{0, b->B}, (int)k1 - 1);
     hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64 * NSTAT), 0, st, b->partials, b->counters, b->stats,

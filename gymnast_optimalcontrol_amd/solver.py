@@ -77,6 +77,10 @@ class BatchedNewtonSolver:
     # at 16,384 lanes, +10% at 24,576, +5.5% at 32,768 (= 2 workgroups per CU), and 10% behind from 36,864 on,
     # where some CUs take a third workgroup (same box, profiles/r02_sched_sweep.log).
     PERSISTENT_MAX_LANES_PER_CU = 128
+    # The straggler tail (gym_newton_tail: one workgroup per lane, every Armijo trial at once) takes over the serial /
+    # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
+    # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.
+    TAIL_LANES_PER_CU = 4
 
     @staticmethod
     def pipeline_min_lanes(device) -> int:
@@ -93,7 +97,7 @@ class BatchedNewtonSolver:
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
                  capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
-                 capture_sigma=(0, 1, 2)):
+                 capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -201,6 +205,16 @@ class BatchedNewtonSolver:
         # sigma of the captured lanes at these iterations (the reference's report plots iterations 0, 1, 2 and the
         # last, trajectory_generation.py:341, 476-480; the last one is the solve's own sigma output)
         self.capture_sigma = tuple(sorted({int(i) for i in (capture_sigma or ())}))
+        # straggler tail (serial / pipelined schedules; needs the full state store, whole-iteration launches: no
+        # trajectory capture, at most 64 Armijo trials): switch once the global active count is <= tail_lanes.
+        # Default: on with the automatic schedule choice; a caller that picks a schedule gets it pure
+        if tail_lanes is None:
+            tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count
+                          if pipeline is None and persistent is None else 0)
+        tail_ok = not self.persistent and not self.checkpoint and self.capture_lanes is None and 1 <= int(max_ls) <= 64
+        self.tail_lanes = int(tail_lanes) if tail_ok else 0
+        self.tail_chunk = max(int(tail_chunk), 1)
+        self._tail_scratch = None
         self._cap_pos = None
         self._cap_log = []
         self._sig_log = []
@@ -265,6 +279,27 @@ class BatchedNewtonSolver:
         _lib.check(self.eng.lib.gym_newton_run(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
                                                C.byref(self.batch), int(k0), int(k1), self.eng.stream),
                    "gym_newton_run")
+
+    def tail_run(self, k0: int, k1: int) -> torch.Tensor:
+        """Iterations k0 .. k1-1 of every lane still active, on the straggler-tail kernel (gym_newton_tail: one
+        workgroup per lane, every Armijo trial at once; the serial schedule's bits).  Every active lane must have
+        done k0 iterations (the lock-step schedules' state after ``k0`` calls of iteration()).  Returns the 8
+        statistics after iteration k1 - 1 (device)."""
+        lanes = (self.status[:self.B] == _lib.ACTIVE).nonzero().flatten().to(torch.int32)
+        n = int(lanes.numel())
+        need = C.c_int64()
+        _lib.check(self.eng.lib.gym_newton_tail_scratch(self.N, n, int(self.armijo.max_ls), C.byref(need)),
+                   "gym_newton_tail_scratch")
+        if self._tail_scratch is None or self._tail_scratch.numel() < need.value:
+            self._tail_scratch = None
+            self._tail_scratch = torch.empty(int(need.value), dtype=F64, device=self.eng.device)
+        sc = self._tail_scratch
+        _lib.check(self.eng.lib.gym_newton_tail(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
+                                                C.byref(self.batch), lanes.data_ptr() if n else None, n,
+                                                sc.data_ptr(), int(sc.numel()), int(k0), int(k1), self.eng.stream),
+                   "gym_newton_tail")
+        self.k = int(k1)
+        return self.stats[:8]
 
     def _phase(self, p: int, do_backward: bool):
         _lib.check(self.eng.lib.gym_newton_phase(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
@@ -524,6 +559,7 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
     all-reduced across ranks (``reduce_stats``, SUM) and read on the host; the loop stops when no
     lane of any rank is active.  Returns the list of host statistics if ``keep_stats``."""
     log = []
+    tail = int(getattr(stepper, "tail_lanes", 0) or 0)
     for k in range(int(max_iters)):
         st = stepper.iteration()
         if (k + 1) % sync_every == 0 or k + 1 == max_iters:
@@ -540,6 +576,33 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
                       f"retry={int(host[4])}", flush=True)
             if host[0] == 0:
                 break
+            # the straggler tail: decided on the (all-reduced) global active count, so every rank switches at the
+            # same iteration and pairs up the same collectives afterwards
+            if tail and host[0] <= tail and k + 1 < max_iters:
+                log += tail_loop(stepper, k + 1, int(max_iters), reduce_stats, log_every, keep_stats)
+                break
+    return log
+
+
+def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep_stats: bool) -> list:
+    """The rest of a serial / pipelined solve on the straggler-tail kernel, ``tail_chunk`` iterations per launch
+    (a lane stops inside a launch when it finishes; the launch ends with its last lane); the statistics are
+    all-reduced and read after each launch, and the loop stops when no lane of any rank is active."""
+    log = []
+    while k < max_iters:
+        k1 = min(max_iters, k + solver.tail_chunk)
+        st = solver.tail_run(k, k1)
+        k = k1
+        if reduce_stats is not None:
+            st = reduce_stats(st)
+        host = st.cpu().numpy()
+        solver.collect_timing()
+        if keep_stats:
+            log.append(host.copy())
+        if log_every:
+            print(f"tail iter {k}: active={int(host[0])} sumJ={host[1]:.6e}", flush=True)
+        if host[0] == 0:
+            break
     return log
 
 

@@ -101,9 +101,9 @@ typedef struct gym_armijo {
 /* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
  * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
  * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p), 7 sigma1 re-run of the lanes that
- * backtrack, 8 persistent run (gym_newton_run).  A pair is recorded only if the previous one of its kind was
- * collected. */
-#define GYM_NK 9
+ * backtrack, 8 persistent run (gym_newton_run), 9 straggler tail (gym_newton_tail).  A pair is recorded only
+ * if the previous one of its kind was collected. */
+#define GYM_NK 10
 typedef struct gym_timing {
     void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
     double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
@@ -237,6 +237,19 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
  * iterations every active lane has done (0 after gym_newton_init).  Not with GYM_FLAG_X_CKPT (GYM_EINVAL). */
 int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t k0,
                    int32_t k1, void* stream);
+/* Straggler tail: the n_lanes lanes of lanes[] (device, each ACTIVE with k0 iterations done) run their own outer
+ * iterations k0 .. k1-1 back to back, ONE workgroup per lane: the sweep stores K row 1, cg and sigma1 in one pass
+ * (the 64 threads linearise 64 stages at a time), then Armijo trials 1..max_ls are evaluated AT ONCE (thread c:
+ * gamma_0 beta^c, into scratch slot c) and the first accepted one becomes the next iterate -- the sequential
+ * search's decision and the serial schedule's bits (newton_Algorithm :329-396 per lane).  Then the statistics of
+ * iteration k1-1 into stats[0,8) over the whole batch.  scratch: device doubles, at least
+ * gym_newton_tail_scratch(N, n_lanes, max_ls); max_ls <= 64; not with GYM_FLAG_X_CKPT (GYM_EINVAL).
+ * Replaces, for the last few lanes of a solve, the per-iteration launches of newton_Algorithm's loop (:329). */
+int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt,
+                    const int32_t* lanes, int32_t n_lanes, double* scratch, int64_t scratch_doubles, int32_t k0,
+                    int32_t k1, void* stream);
+/* [host] Scratch doubles gym_newton_tail needs for n_lanes lanes (candidate trajectories of every trial). */
+int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t* doubles_out);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
  * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
  * (sigma0 recomputed from that iteration's u0).  Any output may be NULL.  With GYM_FLAG_X_CKPT the result

@@ -148,10 +148,16 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
                lib.gym_newton_sigma(R(m), R(w), R(b), D, None),
                lib.gym_newton_fill_states(R(m), R(b), 0, None),
                lib.gym_newton_finalize(R(m), R(w), R(b), 1, D, D, D, D, None),
-               lib.gym_newton_gamma_sweep(R(m), R(w), R(a), R(b), 0, D, 4, D, None)]
-        assert rcs == [1] * 8, (b.B, b.Bp, b.N, b.flags, rcs)
+               lib.gym_newton_gamma_sweep(R(m), R(w), R(a), R(b), 0, D, 4, D, None),
+               lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 1, D, 1 << 40, 0, 1, None)]
+        assert rcs == [1] * 9, (b.B, b.Bp, b.N, b.flags, rcs)
     b = batch()
     assert lib.gym_newton_run(R(m), R(w), R(a), R(b), 5, 1, None) == 1                   # k1 < k0
+    need = C.c_int64()
+    assert lib.gym_newton_tail_scratch(501, 3, 20, C.byref(need)) == 0 and need.value == 64 * (4 * 501 + 2 * 500)
+    assert lib.gym_newton_tail_scratch(501, 3, 65, C.byref(need)) == 1                  # > 64 trials
+    assert lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 3, D, need.value - 1, 0, 1, None) == 1   # scratch short
+    assert lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 3, D, 1 << 40, 4, 2, None) == 1          # k1 < k0
     assert lib.gym_newton_iteration(R(m), R(w), R(_lib.GymArmijo(1e-4, 0.7, 0.5, 0.1, 0, 0)), R(b), 0, None) == 1
     assert lib.gym_rk4_step(R(m), D, D, D, -1, None) == 1 and lib.gym_jacobians(R(m), D, D, D, D, -1, None) == 1
     assert lib.gym_track_rollout(R(m), D, D, D, D, -1, 500, D, D, None) == 1

@@ -1,0 +1,98 @@
+"""The straggler tail (gym_newton_tail: one workgroup per lane, every Armijo trial at once) against the serial
+schedule, bit for bit, through the C-ABI.
+
+Hard lanes (theta0 ~ U(+-1.5), some with initial velocities, gamma_0 = 1 so that most iterations backtrack), a NaN
+lane, lanes that fail the line search and lanes cut off at max_iters.  The tail takes over from the serial schedule
+after the first iteration, from the pipelined schedule mid-solve, and with launches of a few iterations (chunk
+boundaries inside backtracking runs).  Every output must be the serial solve's: trajectories, controls, last
+gains and sigma, costs, step sizes, iteration / rollout counts, statuses and the per-lane histories.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("x", "u", "K", "sigma", "cost", "gamma", "n_iter", "status", "n_rollouts", "hist_cost", "hist_smax")
+
+
+def _hard_lanes(B, seed=5):
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((B, 4))
+    x0[:, :2] = rng.uniform(-1.5, 1.5, (B, 2))
+    x0[::9, 2:] = rng.uniform(-2.0, 2.0, (len(x0[::9]), 2))
+    x0[7] = np.nan
+    x0[0] = 0.0
+    return x0
+
+
+def _same(a, b, name):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, name
+    assert np.array_equal(a, b, equal_nan=True), (name, np.argwhere(~((a == b) | (np.isnan(a) & np.isnan(b))))[:5])
+
+
+def _refs(kind):
+    if kind == "task1":            # live tau1 channel: the general (tau1-streaming) kernels
+        g = load_golden("task1_solve")
+        return g["x_ref"], g["u_ref_full"]
+    from bench import load_refs
+    return load_refs()
+
+
+@pytest.mark.parametrize("kind", ["task2", "task1", "per_lane"])
+def test_straggler_tail_is_bitwise_the_serial_schedule(kind):
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    B, max_iters = 1000, 150
+    x0 = _hard_lanes(B)
+    if kind == "per_lane":
+        xr, ur = _refs("task2")
+        xr = np.broadcast_to(xr, (B,) + xr.shape).copy()
+        ur = np.broadcast_to(ur, (B,) + ur.shape).copy()
+        ur[1::3, :, 1] *= 0.8
+    else:
+        xr, ur = _refs(kind)
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=1.0, max_ls=20, hist_len=max_iters)
+    ref = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=0, **kw)
+    r = ref.solve(x0, max_iters)
+    st = r.status.cpu().numpy()
+    for code in (_lib.CONVERGED, _lib.LS_FAILED, _lib.MAX_ITERS):
+        assert (st == code).any(), (code, np.bincount(st))
+    assert int(st[7]) == _lib.LS_FAILED                       # the NaN lane
+    assert int((r.n_rollouts > r.n_iter).sum()) > 100          # backtracking throughout
+    runs = {
+        "serial->tail at k=1": dict(pipeline=False, tail_lanes=10 ** 9),
+        "pipelined->tail mid-solve, chunk 7": dict(pipeline=True, tail_lanes=400, tail_chunk=7),
+    }
+    for name, skw in runs.items():
+        s = BatchedNewtonSolver(eng, xr, ur, B, **skw, **kw)
+        assert s.tail_lanes > 0
+        t = s.solve(x0, max_iters)
+        assert t.iterations == r.iterations or int(t.n_iter.max()) == int(r.n_iter.max()), name
+        for f in FIELDS:
+            _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{name}: {f}")
+
+
+def test_straggler_tail_on_the_automatic_schedule():
+    """The automatic schedule hands the last lanes to the tail by itself (bench.py's path): a 40,000-lane batch
+    (serial schedule) whose last lanes backtrack, against the same batch with the tail off."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from bench import load_refs
+    xr, ur = load_refs()
+    B = 40000
+    x0 = np.zeros((B, 4))
+    x0[:, :2] = np.random.default_rng(2).uniform(-0.5, 0.5, (B, 2))
+    x0[1:B:997, :2] = np.random.default_rng(3).uniform(-1.5, 1.5, (len(x0[1:B:997]), 2))
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1)
+    auto = BatchedNewtonSolver(eng, xr, ur, B, **kw)
+    assert auto.schedule == "serial" and auto.tail_lanes > 0
+    t = auto.solve(x0, 700)
+    r = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=0, **kw).solve(x0, 700)
+    for f in FIELDS[:9]:
+        _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f)
