@@ -507,6 +507,120 @@ struct Sweep {
     }
 };
 
+// ------------------------------------------------------------------------------------------
+// The Riccati update of Sweep::step_lin on a lane QUAD (lanes 4q .. 4q+3 of a wavefront hold one trajectory).
+// Lane r of the quad owns row r of P (all four entries: the symmetric matrix stored by rows) and p_r.  Per stage:
+//   Pb_r (own row)  ->  Pb and p broadcast in the quad (DPP)  ->  G11, g1, F_r, k_r, sigma1 (every lane the same
+//   uniform values; F_r in lane r)  ->  W row r = (P A_d)_r  ->  k, G11 k and the W rows exchanged through LDS
+//   ->  lane r evaluates row r of the new P: entry (r, j) is nP(min(r, j), max(r, j)), the upper-triangle entry
+//   the single-lane step computes, with the same expression (form and operands gathered per lane from LDS), so
+//   both copies of an off-diagonal entry are its bits  ->  p_r.
+// Every quantity is the single-lane step's expression with the same operands, compiled with FMA contraction
+// inside expressions only: the same bits (the schedules' bitwise tests run it against the single-lane sweep).
+// Where rows 0-1 and rows 2-3 use different forms (A_d rows 0, 1 are e1^T + dt e3^T, e2^T + dt e4^T), both forms
+// are evaluated and the lane's one selected.  About 80 fp64 instructions per lane and stage instead of ~200.
+// ------------------------------------------------------------------------------------------
+constexpr int QX_DOUBLES = 24;   // LDS exchange area per quad: W rows (16), (k_r, G11 k_r) pairs (8)
+template <int CTRL>
+__device__ __forceinline__ double qperm(double v) { return gym::dpp_d<CTRL>(v); }
+template <bool U0Z>
+struct QuadSweep {
+    double R0, R1, R2, R3, pr;   // row r of P, p_r
+    double dJ = 0.0, smax = 0.0;
+    int r;                       // this lane's row (lane & 3)
+    bool hi;                     // r >= 2
+    // per-lane LDS gather offsets of the row-r entries (slot j): W base row / col, A coefficient row i = min(r, j)
+    int ob[4], o2[4], o3[4], oi[4], ok[4];
+    double add[4];               // twoQ_r on the diagonal slot, -0.0 elsewhere (x + -0.0 == x, bit for bit)
+
+    __device__ __forceinline__ QuadSweep(const KW& w, int lane, double2 xa, double2 xb, const double* xrT) {
+        r = lane & 3;
+        hi = r >= 2;
+        const double qt = 2.0 * (r == 0 ? w.QT[0] : r == 1 ? w.QT[1] : r == 2 ? w.QT[2] : w.QT[3]);
+        R0 = r == 0 ? qt : 0.0; R1 = r == 1 ? qt : 0.0; R2 = r == 2 ? qt : 0.0; R3 = r == 3 ? qt : 0.0;
+        const double xv = r == 0 ? xa.x : r == 1 ? xa.y : r == 2 ? xb.x : xb.y;
+        const double xrv = r == 0 ? xrT[0] : r == 1 ? xrT[1] : r == 2 ? xrT[2] : xrT[3];
+        pr = qt * (xv - xrv);    // p_i = P_ii (x_i - xr_i), as the single-lane terminal condition
+        const double tq = r == 0 ? w.twoQ[0] : r == 1 ? w.twoQ[1] : r == 2 ? w.twoQ[2] : w.twoQ[3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = r < j ? r : j, jj = r < j ? j : r;
+            ob[j] = (i >= 2 ? i - 2 : i) * 4 + jj;
+            o2[j] = 8 + jj;
+            o3[j] = 12 + jj;
+            oi[j] = i;
+            ok[j] = jj;
+            add[j] = (r == j) ? tq : -0.0;
+        }
+    }
+
+    // L: the stage's linearisation in LDS (stage_lin's fields in Lin order: A20..A23, A30..A33, bd2, bd3,
+    // q0..q3, r0, r1); X: this quad's exchange area.  Outputs the gain row k0..k3 and sigma (s0, s1) -- uniform.
+    __device__ __forceinline__ void step(const KW& w, const double* L, double dt, double* X, double& k0, double& k1,
+                                         double& k2, double& k3, double& s0, double& s1) {
+#pragma clang fp contract(on)
+        const double bd2 = L[8], bd3 = L[9], r1 = L[15];
+        const double A2r = L[r], A3r = L[4 + r], qr = L[10 + r];
+        const double A20 = L[0], A21 = L[1], A22 = L[2], A23 = L[3];
+        const double A30 = L[4], A31 = L[5], A32 = L[6], A33 = L[7];
+        // Pb = P B_d[:,1]: row r here, then the rows the gain needs from the other lanes of the quad
+        const double Pbr = R2 * bd2 + R3 * bd3;
+        const double Pb2 = qperm<0xAA>(Pbr), Pb3 = qperm<0xFF>(Pbr), Pbh = qperm<0x44>(Pbr);
+        const double p2 = qperm<0xAA>(pr), p3 = qperm<0xFF>(pr), ph = qperm<0x44>(pr);
+        const double G11 = w.twoR1 + (bd2 * Pb2 + bd3 * Pb3);
+        // F row 1 = (P b)^T A_d, entry r (rows 0, 1 of A_d: [1 0 dt 0], [0 1 0 dt])
+        const double Fa = Pbh + A2r * Pb2 + A3r * Pb3;
+        const double Fb = dt * Pbh + A2r * Pb2 + A3r * Pb3;
+        const double F = hi ? Fb : Fa;
+        const double g1 = r1 + (bd2 * p2 + bd3 * p3);
+        const double iG = gym::recip(G11);
+        const double kr = -F * iG;
+        s1 = -g1 * iG;
+        if (U0Z) {
+            s0 = -0.0;
+            const double d1 = g1 * s1;
+            dJ += d1;
+        } else {
+            const double r0 = L[14];
+            s0 = -r0 * w.iG00;
+            dJ += r0 * s0 + g1 * s1;
+        }
+        const double gkr = G11 * kr;
+        // W row r = (P A_d)_r
+        const double W0 = R0 + R2 * A20 + R3 * A30, W1 = R1 + R2 * A21 + R3 * A31;
+        const double W2 = dt * R0 + R2 * A22 + R3 * A32, W3 = dt * R1 + R2 * A23 + R3 * A33;
+        X[16 + 2 * r] = kr; X[17 + 2 * r] = gkr;
+        X[4 * r + 0] = W0; X[4 * r + 1] = W1; X[4 * r + 2] = W2; X[4 * r + 3] = W3;
+        __builtin_amdgcn_wave_barrier();
+        // row r of P <- 2Q + A_d^T W - K^T G K, entry (r, j) = the upper-triangle entry (min, max)
+        double e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double Wb = X[ob[j]], Wt2 = X[o2[j]], Wt3 = X[o3[j]];
+            const double A2 = L[oi[j]], A3 = L[4 + oi[j]];
+            const double gk = X[17 + 2 * oi[j]], kj = X[16 + 2 * ok[j]];
+            double Y;
+            if (j < 2) {   // min(r, j) < 2: every lane uses the rows-0/1 form
+                Y = (Wb + A2 * Wt2 + A3 * Wt3) + add[j];
+            } else {
+                const double Ya = Wb + A2 * Wt2 + A3 * Wt3;
+                const double Yb = dt * Wb + A2 * Wt2 + A3 * Wt3;
+                Y = (hi ? Yb : Ya) + add[j];
+            }
+            e[j] = Y - gk * kj;
+        }
+        // p_r <- q_r + (A_d^T p)_r - k_r G11 sigma1
+        const double gs = G11 * s1;
+        const double npa = qr + (pr + A2r * p2 + A3r * p3) - kr * gs;
+        const double npb = qr + (dt * ph + A2r * p2 + A3r * p3) - kr * gs;
+        k0 = X[16]; k1 = X[18]; k2 = X[20]; k3 = X[22];
+        __builtin_amdgcn_wave_barrier();
+        R0 = e[0]; R1 = e[1]; R2 = e[2]; R3 = e[3];
+        pr = hi ? npb : npa;
+        smax = U0Z ? gym::nanmax_abs(smax, s1) : gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
+    }
+};
+
 // API form: writes K row 1 (pairs), sigma planes and optionally lambda; register prefetch of stage t-1.
 template <bool LAMBDA>
 __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const double2* __restrict__ x,
@@ -2214,9 +2328,14 @@ __device__ __forceinline__ targs_t tail_args() {
     return (targs_t)p;
 }
 
+// GYM_TAIL_QUAD: the tail sweep's Riccati recursion on lane quads (QuadSweep; every quad of the wavefront runs the
+// lane's recursion, the same bits) instead of on every thread (Sweep::step_lin)
+#ifndef GYM_TAIL_QUAD
+#define GYM_TAIL_QUAD 1
+#endif
 // the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage; returns dJ, max|sigma|
 template <bool U0Z, bool RL>
-__device__ __forceinline__ void tail_sweep(double* lin, int lane, int64_t l, int cb, double& dJ_out,
+__device__ __forceinline__ void tail_sweep(double* lin, double* xq, int lane, int64_t l, int cb, double& dJ_out,
                                            double& smax_out) {
     const targs_t R = tail_args();
     const int T = R->N - 1;
@@ -2231,6 +2350,8 @@ __device__ __forceinline__ void tail_sweep(double* lin, int lane, int64_t l, int
     const char* Cb = reinterpret_cast<const char*>(R->cs);
     const double g0 = R->a.gamma0;
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
+    QuadSweep<U0Z> Q(R->w, lane, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
+    double* X = xq + (lane >> 2) * QX_DOUBLES;
     for (int tb = T - 1; tb >= 0; tb -= TL_STAGES) {
         const int t = tb - lane;   // this thread's stage of the pass
         if (t >= 0) {
@@ -2251,24 +2372,28 @@ __device__ __forceinline__ void tail_sweep(double* lin, int lane, int64_t l, int
         for (int i = 0; i < n; ++i) {   // every thread runs the recursion (the same bits); thread 0 stores
             const double* s = lin + i * TL_PITCH;
             const KArgs ka = kernarg_consts();
-            const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
-                        s[10], s[11], s[12], s[13], s[14], s[15], ka.m.h};
             double k0, k1, k2, k3, s0, s1;
-            S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
+            if (GYM_TAIL_QUAD) {
+                Q.step(ka.w, s, ka.m.h, X, k0, k1, k2, k3, s0, s1);
+            } else {
+                const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                            s[10], s[11], s[12], s[13], s[14], s[15], ka.m.h};
+                S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
+            }
             if (lane == 0)
                 store_stage<OUT_ALL>(Kb, Cb, tb - i, row, plane, o2, o1, make_double2(s[16], s[17]),
                                      make_double2(s[18], s[19]), s[20], g0, k0, k1, k2, k3, s1);
         }
         __syncthreads();
     }
-    dJ_out = S.dJ;
-    smax_out = S.smax;
+    dJ_out = GYM_TAIL_QUAD ? Q.dJ : S.dJ;
+    smax_out = GYM_TAIL_QUAD ? Q.smax : S.smax;
 }
 
 // Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) into virtual lane v of the
 // scratch; returns the candidate's cost
-template <bool U0Z, bool RL>
-__device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, double g, int64_t v) {
+template <bool U0Z, bool RL, bool PAIR>
+__device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, double g, int64_t v, bool odd) {
     const targs_t R = tail_args();
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
@@ -2286,10 +2411,13 @@ __device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, doubl
     const double gamma0 = R->a.gamma0, dg = g - gamma0;
     const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
     double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    // PAIR: the candidate's chain on a lane pair (gym::rk4_pair, bit-identical to rk4); the even lane stores
+    // (th1, th2) and the controls, the odd lane (w1, w2)
+    const bool st_a = !PAIR || !odd, st_b = !PAIR || odd;
     {
         const auto rX = rsrc(Xs);
-        bst2(rX, v2, 0, n0, n1);
-        bst2(rX, v2, WROW, n2, n3);
+        if (st_a) bst2(rX, v2, 0, n0, n1);
+        if (st_b) bst2(rX, v2, WROW, n2, n3);
     }
     double J = 0.0;
     auto fetch = [&](TrialStage& q, int t) {
@@ -2315,28 +2443,34 @@ __device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, doubl
         const double u1 = c == 0 ? y : ysig;
         const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = u1 - urt[1];
         J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
-        const auto rO = rsrc(Us + (int64_t)t * srow);
-        if (!U0Z) bst1(rO, v1o, 0, v0);
-        bst1(rO, v1o, splane, u1);
-        gym::rk4(ka.m, n0, n1, n2, n3, u1, pk);
+        if (st_a) {
+            const auto rO = rsrc(Us + (int64_t)t * srow);
+            if (!U0Z) bst1(rO, v1o, 0, v0);
+            bst1(rO, v1o, splane, u1);
+        }
+        if (PAIR)
+            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, u1, pk);
+        else
+            gym::rk4(ka.m, n0, n1, n2, n3, u1, pk);
         const auto rX = rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow));
-        bst2(rX, v2, 0, n0, n1);
-        bst2(rX, v2, WROW, n2, n3);
+        if (st_a) bst2(rX, v2, 0, n0, n1);
+        if (st_b) bst2(rX, v2, WROW, n2, n3);
     }
     const KArgs ka = kernarg_consts();
     return J + xcost(ka.w.QT, n0, n1, n2, n3, xr + 4 * T);
 }
 
-template <bool U0Z, bool RL>
+template <bool U0Z, bool RL, bool PAIR>
 __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
     __shared__ double lin[TL_STAGES * TL_PITCH];
+    __shared__ double xq[(BLK / 4) * QX_DOUBLES];
     const int lane = threadIdx.x;
     const int64_t l = tail_args()->list[blockIdx.x];
     int st = tail_args()->status[l];
     for (int k = tail_args()->k0; st == GYM_ACTIVE && k < tail_args()->k1; ++k) {
         const int cb = k & 1;
         double dJ, sm;
-        tail_sweep<U0Z, RL>(lin, lane, l, cb, dJ, sm);
+        tail_sweep<U0Z, RL>(lin, xq, lane, l, cb, dJ, sm);
         {
             const targs_t Q = tail_args();
             if (lane == 0) {
@@ -2347,18 +2481,20 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         }
         lane_fence();   // K1 / cg / sigma1 of this sweep visible to every thread's loads
         const int max_ls = tail_args()->a.max_ls;
-        const int64_t v = (int64_t)blockIdx.x * max_ls + lane;
+        const int cand = PAIR ? lane >> 1 : lane;   // this thread's trial (PAIR: on lanes 2c, 2c + 1)
+        const int64_t v = (int64_t)blockIdx.x * max_ls + cand;
         double g = tail_args()->a.gamma0;
-        for (int q = 0; q < lane && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
+        for (int q = 0; q < cand && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
         bool ok = false;
         double Jn = 0.0;
-        if (lane < max_ls) {
-            Jn = tail_candidate<U0Z, RL>(l, cb, lane, g, v);
+        if (cand < max_ls) {
+            Jn = tail_candidate<U0Z, RL, PAIR>(l, cb, cand, g, v, lane & 1);
             const targs_t R = tail_args();
             ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
         }
         const unsigned long long acc = __ballot(ok);
-        const int first = acc ? __ffsll((long long)acc) - 1 : -1;   // the first accepted trial, in order
+        // the first accepted trial, in order (PAIR: both lanes of a pair hold the same decision)
+        const int first = acc ? (__ffsll((long long)acc) - 1) / (PAIR ? 2 : 1) : -1;
         const int nr = first >= 0 ? first + 1 : max_ls;
         lane_fence();   // the candidates' scratch stores, before the copy reads them
         if (first >= 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
@@ -2374,8 +2510,9 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
                 }
             }
         }
-        const double Jf = __shfl(Jn, first >= 0 ? first : 0);
-        const double gf = __shfl(g, first >= 0 ? first : 0);
+        const int src = (first >= 0 ? first : 0) * (PAIR ? 2 : 1);
+        const double Jf = __shfl(Jn, src);
+        const double gf = __shfl(g, src);
         if (lane == 0) {
             const targs_t F = tail_args();
             F->n_roll[l] += nr;
@@ -2991,7 +3128,14 @@ int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* 
         ta.sx = (double2*)scratch;
         ta.su = scratch + 4 * (int64_t)b->N * ta.Vp;
         ta.Bp = b->Bp; ta.N = b->N; ta.k0 = k0; ta.k1 = k1; ta.pad = 0;
-        hipLaunchKernelGGL(RUN_SEL(b, k_nt_tail), dim3((unsigned)n_lanes), dim3(BLK), 0, st, ta);
+        // trials on lane pairs while they fit one wavefront (gym::rk4_pair: the same bits, a shorter chain)
+        const bool pair = a->max_ls <= BLK / 2 && !(b->flags & GYM_FLAG_RUN_SINGLE);
+        const bool u0z = b->flags & GYM_FLAG_U0_ZERO, rl = b->flags & GYM_FLAG_REF_LANE;
+        const auto kern = pair ? (rl ? (u0z ? k_nt_tail<true, true, true> : k_nt_tail<false, true, true>)
+                                     : (u0z ? k_nt_tail<true, false, true> : k_nt_tail<false, false, true>))
+                               : (rl ? (u0z ? k_nt_tail<true, true, false> : k_nt_tail<false, true, false>)
+                                     : (u0z ? k_nt_tail<true, false, false> : k_nt_tail<false, false, false>));
+        hipLaunchKernelGGL(kern, dim3((unsigned)n_lanes), dim3(BLK), 0, st, ta);
     }
     // the statistics after iteration k1 - 1, over the whole batch (as gym_newton_run)
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,

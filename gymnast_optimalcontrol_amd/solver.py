@@ -104,6 +104,7 @@ class BatchedNewtonSolver:
         # the largest shard of the global batch, so that every rank picks the same schedule: the schedules
         # synchronise (all-reduce) at different points, and mixed choices would pair up the wrong collectives.
         sched_B = self.B_sched = int(schedule_lanes) if schedule_lanes is not None else int(B)
+        auto_schedule = pipeline is None and persistent is None
         engine.weights.require_gain_solvable()
         self.eng = engine
         self.x_ref, self.u_ref = engine.refs(x_ref, u_ref, per_lane=True)
@@ -210,7 +211,7 @@ class BatchedNewtonSolver:
         # Default: on with the automatic schedule choice; a caller that picks a schedule gets it pure
         if tail_lanes is None:
             tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count
-                          if pipeline is None and persistent is None else 0)
+                          if auto_schedule else 0)
         tail_ok = not self.persistent and not self.checkpoint and self.capture_lanes is None and 1 <= int(max_ls) <= 64
         self.tail_lanes = int(tail_lanes) if tail_ok else 0
         self.tail_chunk = max(int(tail_chunk), 1)

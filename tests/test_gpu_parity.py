@@ -313,7 +313,7 @@ def test_last_iteration_gains_and_sigma_vs_oracle(task2_refs, schedule, max_iter
 @pytest.mark.parametrize("schedule", ["serial", "pipelined", "persistent"])
 @pytest.mark.parametrize("max_iters", [12, 120])
 def test_wide_start_lanes_vs_reference(golden, task2_refs, schedule, max_iters):
-    """16 of those lanes pinned to the REFERENCE itself (tests/golden/wide_lanes.npz: newton_Algorithm with
+    """25 lanes like those pinned to the REFERENCE itself (tests/golden/wide_lanes.npz: newton_Algorithm with
     gamma_0 = 1, tol 1e-4, run in the build container): identical iteration counts, statuses and rollout counts
     (backtracking and the Armijo failure of trajectory_generation.py:352-369), and last-iteration K, sigma, x, u
     per lane within 10x the C restatement's own distance from the reference (no looser than WIDE_TOL)."""

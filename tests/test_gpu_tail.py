@@ -1,8 +1,8 @@
 """The straggler tail (gym_newton_tail: one workgroup per lane, every Armijo trial at once) against the serial
 schedule, bit for bit, through the C-ABI.
 
-Hard lanes (theta0 ~ U(+-1.5), some with initial velocities, gamma_0 = 1 so that most iterations backtrack), a NaN
-lane, lanes that fail the line search and lanes cut off at max_iters.  The tail takes over from the serial schedule
+Hard lanes (theta0 ~ U(+-1.5), some with initial velocities: SURVEY 8(d)'s stress distribution), a NaN lane,
+backtracking lanes, lanes that fail the line search and lanes cut off at max_iters.  The tail takes over from the serial schedule
 after the first iteration, from the pipelined schedule mid-solve, and with launches of a few iterations (chunk
 boundaries inside backtracking runs).  Every output must be the serial solve's: trajectories, controls, last
 gains and sigma, costs, step sizes, iteration / rollout counts, statuses and the per-lane histories.
@@ -46,7 +46,7 @@ def test_straggler_tail_is_bitwise_the_serial_schedule(kind):
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
-    B, max_iters = 1000, 150
+    B, max_iters = 1000, (300 if kind == "task1" else 450)
     x0 = _hard_lanes(B)
     if kind == "per_lane":
         xr, ur = _refs("task2")
@@ -56,17 +56,20 @@ def test_straggler_tail_is_bitwise_the_serial_schedule(kind):
     else:
         xr, ur = _refs(kind)
     eng = AcrobotEngine()
-    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=1.0, max_ls=20, hist_len=max_iters)
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, hist_len=max_iters)
     ref = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=0, **kw)
     r = ref.solve(x0, max_iters)
     st = r.status.cpu().numpy()
-    for code in (_lib.CONVERGED, _lib.LS_FAILED, _lib.MAX_ITERS):
+    # (C oracle, the same lanes: task 2 773 converged / 159 failed / 68 cut off; task 1 43 / 957 / 0)
+    for code in (_lib.CONVERGED, _lib.LS_FAILED) + ((_lib.MAX_ITERS,) if kind != "task1" else ()):
         assert (st == code).any(), (code, np.bincount(st))
     assert int(st[7]) == _lib.LS_FAILED                       # the NaN lane
-    assert int((r.n_rollouts > r.n_iter).sum()) > 100          # backtracking throughout
+    assert int((r.n_rollouts > r.n_iter).sum()) > 100          # backtracking lanes
     runs = {
         "serial->tail at k=1": dict(pipeline=False, tail_lanes=10 ** 9),
         "pipelined->tail mid-solve, chunk 7": dict(pipeline=True, tail_lanes=400, tail_chunk=7),
+        # GYM_FLAG_RUN_SINGLE: every trial's chain on one thread instead of a lane pair
+        "serial->tail, single-lane trials": dict(pipeline=False, tail_lanes=10 ** 9, split_waves=False),
     }
     for name, skw in runs.items():
         s = BatchedNewtonSolver(eng, xr, ur, B, **skw, **kw)
