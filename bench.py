@@ -201,7 +201,7 @@ class NewtonLeg:
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
             schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
-            split_waves=a.split_waves == "on")
+            split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes)
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
@@ -217,16 +217,17 @@ class NewtonLeg:
         gd.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        lane_its, rolls, res = 0, 0, None
+        lane_its, rolls, res, tail_its = 0, 0, None, 0
         for _ in range(steps):
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
             lane_its += res.lane_iterations
             rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
+            tail_its += res.tail_lane_iterations
         torch.cuda.synchronize()
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
-        self.res, self.lane_its, self.steps = res, lane_its, steps
+        self.res, self.lane_its, self.steps, self.tail_lane_its = res, lane_its, steps, tail_its
         self.elapsed = elapsed
         self.lane_its_all = int(gd.sum_over_ranks(lane_its))
         self.rollouts_all = int(gd.sum_over_ranks(rolls))
@@ -253,13 +254,15 @@ class NewtonLeg:
             kern["run"]["achieved_GBs"] = per_launch / (kern["run"]["avg_ms"] * 1e-3) / 1e9
             bytes_per_lane, unit_note = ab["iteration"], "sweep + trial of one lane-iteration"
         elif "phase_odd" in kern:
-            # pipelined schedule: every lane-iteration = one sweep + one trial, all inside the phase launches
-            # (2 * iterations + 1 per solve; a launch's time is recorded whenever its timing slot is free)
+            # pipelined schedule: every lane-iteration = one sweep + one trial inside the phase launches (2 per
+            # outer iteration + 1 per solve; a launch's time is recorded whenever its timing slot is free) -- up to
+            # the straggler tail, whose lane-iterations are not in them
             dom = "phase"
             rec_ms = sum(kern[k]["avg_ms"] * kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
             rec_n = sum(kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
-            total_launches = self.steps * (2 * self.res.iterations + 1)
-            per_launch = lane_its * ab["iteration"] / total_launches
+            total_launches = solver.launches["phase"]
+            tail_its = self.tail_lane_its
+            per_launch = (lane_its - tail_its) * ab["iteration"] / total_launches
             kern["phase"] = {"avg_ms": rec_ms / rec_n, "launches": total_launches, "recorded": rec_n,
                              "algorithmic_bytes_per_launch": per_launch}
             kern["phase"]["achieved_GBs"] = per_launch / (kern["phase"]["avg_ms"] * 1e-3) / 1e9
@@ -374,6 +377,9 @@ def main():
                     help="solver schedule (auto: the solver's choice for the batch size)")
     ap.add_argument("--chunk", type=int, default=128,
                     help="persistent schedule: iterations per launch (0: all of max_iters in one)")
+    ap.add_argument("--tail-lanes", type=int, default=None,
+                    help="straggler tail: hand the last lanes to gym_newton_tail once at most this many are active "
+                         "(default: the solver's, 4 per CU; 0 = off)")
     ap.add_argument("--split-waves", choices=("on", "off"), default="on",
                     help="persistent schedule: two wavefronts per 64 lanes (k_nt_run2, default) or one (k_nt_run)")
     ap.add_argument("--dry-run", action="store_true",
@@ -477,6 +483,13 @@ def main():
            "dist": {"backend": gd.backend_name(), "world_size": gd.rank_world()[1],
                     "launcher": os.environ.get("GYM_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else None)}}
     out["rollouts_per_s"] = main_leg.rollouts_all / main_leg.elapsed   # closed-loop Armijo rollouts, all ranks
+    sv = main_leg.solver
+    out["straggler_tail"] = {
+        "lanes_threshold": sv.tail_lanes, "launches": sv.launches["tail"],
+        "lane_iterations_per_step": main_leg.tail_lane_its // max(a.steps, 1),
+        "share_of_lane_iterations": main_leg.tail_lane_its / max(main_leg.lane_its, 1),
+        "note": "gym_newton_tail: once at most lanes_threshold lanes are active (all ranks), one workgroup per lane, "
+                "every Armijo trial at once (bitwise the serial schedule, tests/test_gpu_tail.py)"}
 
     kern, roof = main_leg.kernel_report(N)
     if kern and rank == 0:

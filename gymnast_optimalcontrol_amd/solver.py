@@ -62,6 +62,7 @@ class SolveResult:
     cost0: dict | None = None               # {lane: J_0} of the captured lanes
     sigmas: dict | None = None              # {lane: {iteration: sigma (T,2)}} of the captured lanes (capture_sigma)
     schedule: str = ""                      # "serial" | "pipelined" | "persistent"
+    tail_lane_iterations: int = 0           # lane-iterations run by the straggler tail (gym_newton_tail)
 
 
 class BatchedNewtonSolver:
@@ -192,6 +193,7 @@ class BatchedNewtonSolver:
         self.batch = b
         self.k = 0
         self.timing = None
+        self.launches = {"phase": 0, "run": 0, "tail": 0, "iteration": 0}   # launches since reset_timing()
         # selected-lane trajectory capture (the reference's history['x_trajs'], trajectory_generation.py:322-327,
         # 387-388): after every iteration the captured lanes' current iterates are gathered on the device; the
         # persistent schedule then runs one iteration per launch.  Not combined with checkpointing (the state
@@ -216,6 +218,7 @@ class BatchedNewtonSolver:
         self.tail_lanes = int(tail_lanes) if tail_ok else 0
         self.tail_chunk = max(int(tail_chunk), 1)
         self._tail_scratch = None
+        self.tail_lane_its = 0
         self._cap_pos = None
         self._cap_log = []
         self._sig_log = []
@@ -234,6 +237,7 @@ class BatchedNewtonSolver:
         return self
 
     def reset_timing(self):
+        self.launches = {"phase": 0, "run": 0, "tail": 0, "iteration": 0}
         if self.timing is not None:
             for i in range(len(_lib.KERNEL_KINDS)):
                 self.timing.ms[i] = 0.0
@@ -277,6 +281,7 @@ class BatchedNewtonSolver:
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
 
     def _run(self, k0: int, k1: int):
+        self.launches["run"] += 1
         _lib.check(self.eng.lib.gym_newton_run(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
                                                C.byref(self.batch), int(k0), int(k1), self.eng.stream),
                    "gym_newton_run")
@@ -295,6 +300,7 @@ class BatchedNewtonSolver:
             self._tail_scratch = None
             self._tail_scratch = torch.empty(int(need.value), dtype=F64, device=self.eng.device)
         sc = self._tail_scratch
+        self.launches["tail"] += 1
         _lib.check(self.eng.lib.gym_newton_tail(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
                                                 C.byref(self.batch), lanes.data_ptr() if n else None, n,
                                                 sc.data_ptr(), int(sc.numel()), int(k0), int(k1), self.eng.stream),
@@ -303,6 +309,7 @@ class BatchedNewtonSolver:
         return self.stats[:8]
 
     def _phase(self, p: int, do_backward: bool):
+        self.launches["phase"] += 1
         _lib.check(self.eng.lib.gym_newton_phase(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
                                                  C.byref(self.batch), p, int(do_backward), self.eng.stream),
                    "gym_newton_phase")
@@ -317,6 +324,7 @@ class BatchedNewtonSolver:
             self._phase(2 * k + 1, True)         # sweep H1 (iteration k) beside trial H0 (iteration k)
             self._phase(2 * k + 2, more)         # sweep H0 (iteration k+1) beside trial H1 (iteration k)
         else:
+            self.launches["iteration"] += 1
             _lib.check(self.eng.lib.gym_newton_iteration(C.byref(self.eng.model), C.byref(self.eng._w),
                                                          C.byref(self.armijo), C.byref(self.batch), k,
                                                          self.eng.stream), "gym_newton_iteration")
@@ -465,6 +473,7 @@ class BatchedNewtonSolver:
             inv = torch.empty_like(perm)
             inv[perm] = torch.arange(self.B, device=perm.device)
             self._capture_start(inv[torch.as_tensor(self.capture_lanes, device=perm.device)].tolist())
+        self.tail_lane_its = 0
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:
@@ -495,6 +504,7 @@ class BatchedNewtonSolver:
         res["cost0"] = self.captured_initial_costs() if self.capture_lanes is not None else None
         res["sigmas"] = self.captured_sigmas() if self.capture_lanes is not None else None
         res["schedule"] = self.schedule
+        res["tail_lane_iterations"] = int(self.tail_lane_its)
         return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
                            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)
 
@@ -548,6 +558,7 @@ def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_ever
             print(f"iter {k}: active={int(host[0])} sumJ={host[1]:.6e} ran={int(host[3])}", flush=True)
         if host[0] == 0:
             break
+    solver.tail_lane_its = int(solver.n_iter[:solver.B].sum().item()) - its0
     return log
 
 
@@ -590,6 +601,7 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
     (a lane stops inside a launch when it finishes; the launch ends with its last lane); the statistics are
     all-reduced and read after each launch, and the loop stops when no lane of any rank is active."""
     log = []
+    its0 = int(solver.n_iter[:solver.B].sum().item())
     while k < max_iters:
         k1 = min(max_iters, k + solver.tail_chunk)
         st = solver.tail_run(k, k1)
