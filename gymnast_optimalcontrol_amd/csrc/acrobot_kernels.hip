@@ -556,8 +556,8 @@ struct QuadSweep {
 
     // L: the stage's linearisation in LDS (stage_lin's fields in Lin order: A20..A23, A30..A33, bd2, bd3,
     // q0..q3, r0, r1); X: this quad's exchange area.  Outputs the gain row k0..k3 and sigma (s0, s1) -- uniform.
-    __device__ __forceinline__ void step(const KW& w, const double* L, double dt, double* X, double& k0, double& k1,
-                                         double& k2, double& k3, double& s0, double& s1) {
+    __device__ __forceinline__ void step(double twoR1, double iG00, const double* L, double dt, double* X, double& k0,
+                                         double& k1, double& k2, double& k3, double& s0, double& s1) {
 #pragma clang fp contract(on)
         const double bd2 = L[8], bd3 = L[9], r1 = L[15];
         const double A2r = L[r], A3r = L[4 + r], qr = L[10 + r];
@@ -567,7 +567,7 @@ struct QuadSweep {
         const double Pbr = R2 * bd2 + R3 * bd3;
         const double Pb2 = qperm<0xAA>(Pbr), Pb3 = qperm<0xFF>(Pbr), Pbh = qperm<0x44>(Pbr);
         const double p2 = qperm<0xAA>(pr), p3 = qperm<0xFF>(pr), ph = qperm<0x44>(pr);
-        const double G11 = w.twoR1 + (bd2 * Pb2 + bd3 * Pb3);
+        const double G11 = twoR1 + (bd2 * Pb2 + bd3 * Pb3);
         // F row 1 = (P b)^T A_d, entry r (rows 0, 1 of A_d: [1 0 dt 0], [0 1 0 dt])
         const double Fa = Pbh + A2r * Pb2 + A3r * Pb3;
         const double Fb = dt * Pbh + A2r * Pb2 + A3r * Pb3;
@@ -582,7 +582,7 @@ struct QuadSweep {
             dJ += d1;
         } else {
             const double r0 = L[14];
-            s0 = -r0 * w.iG00;
+            s0 = -r0 * iG00;
             dJ += r0 * s0 + g1 * s1;
         }
         const double gkr = G11 * kr;
@@ -665,18 +665,23 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const d
 enum SweepOut { OUT_SOLVER = 0, OUT_SIGMA = 1, OUT_ALL = 2 };
 
 // stage t's sweep outputs: K row 1 (wave-blocked pairs), cg (plane 0 of cs), sigma1 (plane 1)
+// the stage's offset cg = (u1 - K1 x) + gamma0 sigma1 (FMA contraction inside the expression only)
+__device__ __forceinline__ double stage_cg(double2 xa, double2 xb, double ut1, double g0, double k0, double k1,
+                                           double k2, double k3, double s1) {
+#pragma clang fp contract(on)
+    const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
+    return __builtin_fma(g0, s1, c1);
+}
 template <int OUT>
 __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int t, uint32_t row, uint32_t plane,
                                             uint32_t o2, uint32_t o1, double2 xa, double2 xb, double ut1, double g0,
                                             double k0, double k1, double k2, double k3, double s1) {
     const auto rC = rsrc(Cb + (int64_t)t * row);
     if (OUT != OUT_SIGMA) {
-#pragma clang fp contract(on)
-        const double c1 = ut1 - (((k0 * xa.x + k1 * xa.y) + k2 * xb.x) + k3 * xb.y);
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
         bst2(rK, o2, 0, k0, k1);
         bst2(rK, o2, WROW, k2, k3);
-        bst1(rC, o1, 0, __builtin_fma(g0, s1, c1));
+        bst1(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
     }
     if (OUT != OUT_SOLVER) bst1(rC, o1, plane, s1);
 }
@@ -1694,6 +1699,8 @@ __device__ __forceinline__ void lane_fence() {   // this lane's stores visible t
 // Diagnostic build only (tools/run2_trace.py): per workgroup and wavefront role, cycles (s_memtime) spent in the
 // sweep, the trial and the post-trial part, accumulated in registers and written once at the kernel's end.
 __device__ unsigned long long g_run2_trace[8192][2][6];
+#endif
+#if defined(GYM_RUN2_TRACE) || defined(GYM_TAIL_TRACE)
 #define R2T_NOW() __builtin_amdgcn_s_memtime()
 #else
 #define R2T_NOW() 0ull
@@ -2333,10 +2340,18 @@ __device__ __forceinline__ targs_t tail_args() {
 #ifndef GYM_TAIL_QUAD
 #define GYM_TAIL_QUAD 1
 #endif
-// the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage; returns dJ, max|sigma|
+// The trials' per-stage inputs are staged in LDS by the sweep (K row 1, cg, sigma1 and u0: 8 doubles per stage), so
+// the trial loop issues no global loads: its scratch stores are never waited on (the GFX9 vmcnt counts both)
+constexpr int TL_TST = 8;
+constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / exchange areas within 56 KiB of LDS
+constexpr size_t tail_lds_bytes(int T) {
+    return sizeof(double) * ((size_t)TL_STAGES * TL_PITCH + (size_t)(BLK / 4) * QX_DOUBLES + (size_t)T * TL_TST);
+}
+// the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage (global, and staged in tst); returns dJ,
+// max|sigma|
 template <bool U0Z, bool RL>
-__device__ __forceinline__ void tail_sweep(double* lin, double* xq, int lane, int64_t l, int cb, double& dJ_out,
-                                           double& smax_out) {
+__device__ __forceinline__ void tail_sweep(double* lin, double* xq, double* tst, int lane, int64_t l, int cb,
+                                           double& dJ_out, double& smax_out) {
     const targs_t R = tail_args();
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
@@ -2349,6 +2364,7 @@ __device__ __forceinline__ void tail_sweep(double* lin, double* xq, int lane, in
     const char* Kb = reinterpret_cast<const char*>(R->K1);
     const char* Cb = reinterpret_cast<const char*>(R->cs);
     const double g0 = R->a.gamma0;
+    const double twoR1 = R->w.twoR1, iG00 = R->w.iG00, dt = R->m.h;   // loop-invariant (no kernarg reloads)
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     QuadSweep<U0Z> Q(R->w, lane, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     double* X = xq + (lane >> 2) * QX_DOUBLES;
@@ -2366,23 +2382,34 @@ __device__ __forceinline__ void tail_sweep(double* lin, double* xq, int lane, in
             s[8] = L.bd2; s[9] = L.bd3; s[10] = L.q0; s[11] = L.q1;
             s[12] = L.q2; s[13] = L.q3; s[14] = L.r0; s[15] = L.r1;
             s[16] = xa.x; s[17] = xa.y; s[18] = xb.x; s[19] = xb.y; s[20] = u1;
+            tst[t * TL_TST + 6] = u0;
         }
         __syncthreads();
         const int n = tb + 1 < TL_STAGES ? tb + 1 : TL_STAGES;
         for (int i = 0; i < n; ++i) {   // every thread runs the recursion (the same bits); thread 0 stores
             const double* s = lin + i * TL_PITCH;
-            const KArgs ka = kernarg_consts();
             double k0, k1, k2, k3, s0, s1;
             if (GYM_TAIL_QUAD) {
-                Q.step(ka.w, s, ka.m.h, X, k0, k1, k2, k3, s0, s1);
+                Q.step(twoR1, iG00, s, dt, X, k0, k1, k2, k3, s0, s1);
             } else {
+                const KArgs ka = kernarg_consts();
                 const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
-                            s[10], s[11], s[12], s[13], s[14], s[15], ka.m.h};
+                            s[10], s[11], s[12], s[13], s[14], s[15], dt};
                 S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
             }
-            if (lane == 0)
-                store_stage<OUT_ALL>(Kb, Cb, tb - i, row, plane, o2, o1, make_double2(s[16], s[17]),
-                                     make_double2(s[18], s[19]), s[20], g0, k0, k1, k2, k3, s1);
+            const double2 xa = make_double2(s[16], s[17]), xb = make_double2(s[18], s[19]);
+            if (lane == 0) {
+                const int ts = tb - i;
+                const double cg = stage_cg(xa, xb, s[20], g0, k0, k1, k2, k3, s1);
+                double* q = tst + ts * TL_TST;
+                q[0] = k0; q[1] = k1; q[2] = k2; q[3] = k3; q[4] = cg; q[5] = s1;
+                const auto rC = rsrc(Cb + (int64_t)ts * row);
+                const auto rK = rsrc(Kb + (int64_t)ts * (2 * (int64_t)row));
+                bst2(rK, o2, 0, k0, k1);
+                bst2(rK, o2, WROW, k2, k3);
+                bst1(rC, o1, 0, cg);
+                bst1(rC, o1, plane, s1);
+            }
         }
         __syncthreads();
     }
@@ -2391,21 +2418,17 @@ __device__ __forceinline__ void tail_sweep(double* lin, double* xq, int lane, in
 }
 
 // Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) into virtual lane v of the
-// scratch; returns the candidate's cost
+// scratch, its streams from the staging tst; returns the candidate's cost
 template <bool U0Z, bool RL, bool PAIR>
-__device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, double g, int64_t v, bool odd) {
+__device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, int cb, int c, double g, int64_t v,
+                                                 bool odd) {
     const targs_t R = tail_args();
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
     const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
     const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
-    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const uint32_t v2 = wbo(v, 2), v1o = (uint32_t)v * 8u;
     const uint32_t srow = (uint32_t)R->Vp * 16u, splane = (uint32_t)R->Vp * 8u;
-    const char* Kb = reinterpret_cast<const char*>(R->K1);
-    const char* Cb = reinterpret_cast<const char*>(R->cs);
-    const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
     const char* Xs = reinterpret_cast<const char*>(R->sx);
     const char* Us = reinterpret_cast<const char*>(R->su);
     const double gamma0 = R->a.gamma0, dg = g - gamma0;
@@ -2420,57 +2443,63 @@ __device__ __forceinline__ double tail_candidate(int64_t l, int cb, int c, doubl
         if (st_b) bst2(rX, v2, WROW, n2, n3);
     }
     double J = 0.0;
-    auto fetch = [&](TrialStage& q, int t) {
-        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        q.k0 = bld2<0>(rK, o2, 0);
-        q.k1 = bld2<0>(rK, o2, WROW);
-        const auto rC = rsrc(Cb + (int64_t)t * row);
-        q.cg = bld1<0>(rC, o1, 0);
-        q.s1 = bld1<0>(rC, o1, plane);
-        q.u0 = U0Z ? 0.0 : bld1<0>(rsrc(Ub + (int64_t)t * row), o1, 0);
-    };
     const gym::PolyRegs pk = gym::poly_vgprs();
-    TrialStage pre;
-    fetch(pre, 0);
+    const KArgs ka = kernarg_consts();
+    const Dyn m = ka.m;
+    const double G00 = ka.w.G00, iG00 = ka.w.iG00;
     for (int t = 0; t < T; ++t) {
-        const TrialStage q = pre;
-        if (t + 1 < T) fetch(pre, t + 1);
-        const double* urt = ur + 2 * t;
-        const KArgs ka = kernarg_consts();
-        const double v0 = U0Z ? 0.0 : trial_u0(q.u0, urt[0], g, ka.w.G00, ka.w.iG00);
-        const double y = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
-        const double ysig = __builtin_fma(dg, q.s1, y);                 // trial_u1_sig's value
+        const double* q = tst + t * TL_TST;
+        const double2 k0 = make_double2(q[0], q[1]), k1 = make_double2(q[2], q[3]);
+        const double cg = q[4], s1 = q[5];
+        const Row<2> urt = ref_row<2, RL>(ur, t);
+        const Row<4> xrt = ref_row<4, RL>(xr, t);
+        const double v0 = U0Z ? 0.0 : trial_u0(q[6], urt.v[0], g, G00, iG00);
+        const double y = trial_u1(k0, k1, cg, n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
+        const double ysig = __builtin_fma(dg, s1, y);            // trial_u1_sig's value
         const double u1 = c == 0 ? y : ysig;
-        const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = u1 - urt[1];
-        J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
+        const double f0 = U0Z ? 0.0 : v0 - urt.v[0], f1 = u1 - urt.v[1];
+        const KArgs kc = kernarg_consts();
+        J = stage_cost<U0Z>(J, kc.w.Q, kc.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
         if (st_a) {
             const auto rO = rsrc(Us + (int64_t)t * srow);
             if (!U0Z) bst1(rO, v1o, 0, v0);
             bst1(rO, v1o, splane, u1);
         }
         if (PAIR)
-            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, u1, pk);
+            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
         else
-            gym::rk4(ka.m, n0, n1, n2, n3, u1, pk);
+            gym::rk4(m, n0, n1, n2, n3, u1, pk);
         const auto rX = rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow));
         if (st_a) bst2(rX, v2, 0, n0, n1);
         if (st_b) bst2(rX, v2, WROW, n2, n3);
     }
-    const KArgs ka = kernarg_consts();
-    return J + xcost(ka.w.QT, n0, n1, n2, n3, xr + 4 * T);
+    const Row<4> xrT = ref_row<4, RL>(xr, T);
+    return J + xcost(ka.w.QT, n0, n1, n2, n3, xrT.v);
 }
 
+#ifdef GYM_TAIL_TRACE
+// Diagnostic build only (tools/tail_trace.py): per workgroup, cycles (s_memtime) in the sweep, the trials, the rest
+// of the iteration, and the iterations run
+__device__ unsigned long long g_tail_trace[4096][4];
+#endif
 template <bool U0Z, bool RL, bool PAIR>
 __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
-    __shared__ double lin[TL_STAGES * TL_PITCH];
-    __shared__ double xq[(BLK / 4) * QX_DOUBLES];
+    extern __shared__ double tail_lds[];          // tail_lds_bytes(T): linearisations, quad exchange, trial staging
+    double* lin = tail_lds;
+    double* xq = lin + TL_STAGES * TL_PITCH;
+    double* tst = xq + (BLK / 4) * QX_DOUBLES;
     const int lane = threadIdx.x;
     const int64_t l = tail_args()->list[blockIdx.x];
     int st = tail_args()->status[l];
+    unsigned long long acc[4] = {0, 0, 0, 0};   // GYM_TAIL_TRACE only
     for (int k = tail_args()->k0; st == GYM_ACTIVE && k < tail_args()->k1; ++k) {
         const int cb = k & 1;
         double dJ, sm;
-        tail_sweep<U0Z, RL>(lin, xq, lane, l, cb, dJ, sm);
+        unsigned long long tt = R2T_NOW();
+        ++acc[3];
+        tail_sweep<U0Z, RL>(lin, xq, tst, lane, l, cb, dJ, sm);
+        acc[0] += R2T_NOW() - tt;
+        tt = R2T_NOW();
         {
             const targs_t Q = tail_args();
             if (lane == 0) {
@@ -2479,7 +2508,7 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
                 if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = sm;
             }
         }
-        lane_fence();   // K1 / cg / sigma1 of this sweep visible to every thread's loads
+        __syncthreads();   // the staged trial inputs (LDS) complete
         const int max_ls = tail_args()->a.max_ls;
         const int cand = PAIR ? lane >> 1 : lane;   // this thread's trial (PAIR: on lanes 2c, 2c + 1)
         const int64_t v = (int64_t)blockIdx.x * max_ls + cand;
@@ -2488,25 +2517,47 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         bool ok = false;
         double Jn = 0.0;
         if (cand < max_ls) {
-            Jn = tail_candidate<U0Z, RL, PAIR>(l, cb, cand, g, v, lane & 1);
+            Jn = tail_candidate<U0Z, RL, PAIR>(tst, l, cb, cand, g, v, lane & 1);
             const targs_t R = tail_args();
             ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
         }
-        const unsigned long long acc = __ballot(ok);
+        const unsigned long long okm = __ballot(ok);
+        acc[1] += R2T_NOW() - tt;
+        tt = R2T_NOW();
         // the first accepted trial, in order (PAIR: both lanes of a pair hold the same decision)
-        const int first = acc ? (__ffsll((long long)acc) - 1) / (PAIR ? 2 : 1) : -1;
+        const int first = okm ? (__ffsll((long long)okm) - 1) / (PAIR ? 2 : 1) : -1;
         const int nr = first >= 0 ? first + 1 : max_ls;
         lane_fence();   // the candidates' scratch stores, before the copy reads them
         if (first >= 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
             const targs_t R = tail_args();
             const int T = R->N - 1;
             const int64_t vf = (int64_t)blockIdx.x * max_ls + first;
-            for (int t = lane; t <= T; t += BLK) {
-                R->x[cb ^ 1][wix(t, 0, 2, l, R->Bp)] = R->sx[wix(t, 0, 2, vf, R->Vp)];
-                R->x[cb ^ 1][wix(t, 1, 2, l, R->Bp)] = R->sx[wix(t, 1, 2, vf, R->Vp)];
-                if (t < T) {
-                    if (!U0Z) R->u[cb ^ 1][pix(t, 0, 2, l, R->Bp)] = R->su[pix(t, 0, 2, vf, R->Vp)];
-                    R->u[cb ^ 1][pix(t, 1, 2, l, R->Bp)] = R->su[pix(t, 1, 2, vf, R->Vp)];
+            for (int t0 = 0; t0 <= T; t0 += 4 * BLK) {   // four knots per thread in flight
+                double2 a[4], b[4];
+                double c0[4], c1[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = t0 + j * BLK + lane;
+                    if (t <= T) {
+                        a[j] = R->sx[wix(t, 0, 2, vf, R->Vp)];
+                        b[j] = R->sx[wix(t, 1, 2, vf, R->Vp)];
+                    }
+                    if (t < T) {
+                        c0[j] = U0Z ? 0.0 : R->su[pix(t, 0, 2, vf, R->Vp)];
+                        c1[j] = R->su[pix(t, 1, 2, vf, R->Vp)];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = t0 + j * BLK + lane;
+                    if (t <= T) {
+                        R->x[cb ^ 1][wix(t, 0, 2, l, R->Bp)] = a[j];
+                        R->x[cb ^ 1][wix(t, 1, 2, l, R->Bp)] = b[j];
+                    }
+                    if (t < T) {
+                        if (!U0Z) R->u[cb ^ 1][pix(t, 0, 2, l, R->Bp)] = c0[j];
+                        R->u[cb ^ 1][pix(t, 1, 2, l, R->Bp)] = c1[j];
+                    }
                 }
             }
         }
@@ -2527,7 +2578,12 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         st = first < 0 ? GYM_LS_FAILED : (sm < tail_args()->a.tol ? GYM_CONVERGED : GYM_ACTIVE);
         lane_fence();   // the next iterate and the lane's state visible to the next iteration
         __syncthreads();
+        acc[2] += R2T_NOW() - tt;
     }
+#ifdef GYM_TAIL_TRACE
+    if (lane == 0 && blockIdx.x < 4096)
+        for (int i = 0; i < 4; ++i) g_tail_trace[blockIdx.x][i] += acc[i];
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3094,7 +3150,7 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
 }
 
 int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t* doubles_out) {
-    if (!doubles_out || N < 2 || n_lanes < 0 || max_ls < 1 || max_ls > BLK) return GYM_EINVAL;
+    if (!doubles_out || N < 2 || N - 1 > TL_MAX_T || n_lanes < 0 || max_ls < 1 || max_ls > BLK) return GYM_EINVAL;
     const int64_t v = (int64_t)n_lanes * max_ls;
     const int64_t Vp = v > 0 ? (v + BLK - 1) / BLK * BLK : BLK;
     *doubles_out = Vp * (4 * (int64_t)N + 2 * (int64_t)(N - 1));
@@ -3135,7 +3191,7 @@ int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* 
                                      : (u0z ? k_nt_tail<true, false, true> : k_nt_tail<false, false, true>))
                                : (rl ? (u0z ? k_nt_tail<true, true, false> : k_nt_tail<false, true, false>)
                                      : (u0z ? k_nt_tail<true, false, false> : k_nt_tail<false, false, false>));
-        hipLaunchKernelGGL(kern, dim3((unsigned)n_lanes), dim3(BLK), 0, st, ta);
+        hipLaunchKernelGGL(kern, dim3((unsigned)n_lanes), dim3(BLK), tail_lds_bytes(b->N - 1), st, ta);
     }
     // the statistics after iteration k1 - 1, over the whole batch (as gym_newton_run)
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
@@ -3227,6 +3283,15 @@ int gym_newton_gamma_sweep(const gym_model* m, const gym_weights* w, const gym_a
     return launch_status();
 }
 
+#ifdef GYM_TAIL_TRACE
+int gym_debug_tail_trace(void* host_out, int reset) {   // diagnostic build only: 4096 x 4 uint64
+    if (reset) {
+        static unsigned long long zero[4096][4];
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_tail_trace), zero, sizeof(zero));
+    }
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tail_trace), sizeof(g_tail_trace));
+}
+#endif
 #ifdef GYM_RUN2_TRACE
 int gym_debug_run2_trace(void* host_out, int reset) {   // diagnostic build only: 8192 x 2 x 6 uint64
     if (reset) {

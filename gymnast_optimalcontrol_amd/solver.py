@@ -192,6 +192,7 @@ class BatchedNewtonSolver:
         b.hist_smax = _lib.ptr(self.hist_smax)
         self.batch = b
         self.k = 0
+        self.timeline = None     # diagnostics: a list records (iterations, active lanes, host time) per sync
         self.timing = None
         self.launches = {"phase": 0, "run": 0, "tail": 0, "iteration": 0}   # launches since reset_timing()
         # selected-lane trajectory capture (the reference's history['x_trajs'], trajectory_generation.py:322-327,
@@ -214,7 +215,9 @@ class BatchedNewtonSolver:
         if tail_lanes is None:
             tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count
                           if auto_schedule else 0)
-        tail_ok = not self.persistent and not self.checkpoint and self.capture_lanes is None and 1 <= int(max_ls) <= 64
+        need = C.c_int64()   # the tail kernel's limits: at most 64 trials, horizons up to its LDS staging
+        tail_ok = (not self.persistent and not self.checkpoint and self.capture_lanes is None and
+                   engine.lib.gym_newton_tail_scratch(self.N, 1, int(max_ls), C.byref(need)) == 0)
         self.tail_lanes = int(tail_lanes) if tail_ok else 0
         self.tail_chunk = max(int(tail_chunk), 1)
         self._tail_scratch = None
@@ -558,7 +561,6 @@ def run_loop(solver: BatchedNewtonSolver, max_iters: int, reduce_stats, log_ever
             print(f"iter {k}: active={int(host[0])} sumJ={host[1]:.6e} ran={int(host[3])}", flush=True)
         if host[0] == 0:
             break
-    solver.tail_lane_its = int(solver.n_iter[:solver.B].sum().item()) - its0
     return log
 
 
@@ -583,6 +585,8 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
                 collect()
             if keep_stats:
                 log.append(host.copy())
+            if getattr(stepper, "timeline", None) is not None:   # diagnostics: (iterations, active, host time)
+                stepper.timeline.append((k + 1, int(host[0]), time.perf_counter()))
             if log_every and (k % log_every == 0):
                 print(f"iter {k}: active={int(host[0])} sumJ={host[1]:.6e} ran={int(host[3])} "
                       f"retry={int(host[4])}", flush=True)
@@ -612,10 +616,13 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
         solver.collect_timing()
         if keep_stats:
             log.append(host.copy())
+        if getattr(solver, "timeline", None) is not None:
+            solver.timeline.append((k, int(host[0]), time.perf_counter()))
         if log_every:
             print(f"tail iter {k}: active={int(host[0])} sumJ={host[1]:.6e}", flush=True)
         if host[0] == 0:
             break
+    solver.tail_lane_its = int(solver.n_iter[:solver.B].sum().item()) - its0
     return log
 
 
