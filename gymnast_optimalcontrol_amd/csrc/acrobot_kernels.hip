@@ -2335,10 +2335,11 @@ __device__ __forceinline__ targs_t tail_args() {
     return (targs_t)p;
 }
 
-// GYM_TAIL_QUAD: the tail sweep's Riccati recursion on lane quads (QuadSweep; every quad of the wavefront runs the
-// lane's recursion, the same bits) instead of on every thread (Sweep::step_lin)
+// GYM_TAIL_QUAD (measurement variant): the tail sweep's Riccati recursion on lane quads (QuadSweep; every quad of
+// the wavefront runs the lane's recursion, the same bits) instead of on every thread (Sweep::step_lin).  Measured
+// slower (latency-bound exchanges), so off by default.
 #ifndef GYM_TAIL_QUAD
-#define GYM_TAIL_QUAD 1
+#define GYM_TAIL_QUAD 0
 #endif
 // The trials' per-stage inputs are staged in LDS by the sweep (K row 1, cg, sigma1 and u0: 8 doubles per stage), so
 // the trial loop issues no global loads: its scratch stores are never waited on (the GFX9 vmcnt counts both)
