@@ -240,3 +240,49 @@ def test_bench_refuses_a_world_size_mismatch():
     assert rc == 2 and out is None and "WORLD_SIZE=1" in err
     rc, out, _ = _bench(["--gpus", "1", "--dry-run"])
     assert rc == 0 and out["n_gpus"] == 1 and out["dist"]["world_size"] == 1 and out["dist"]["backend"] is None
+
+
+# ------------------------------------------------------------------ the straggler-tail switch across ranks
+def _tail_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from gymnast_optimalcontrol_amd import distributed as gd
+    from gymnast_optimalcontrol_amd.solver import newton_loop
+    from host_loop_mock import MockSolver
+    gd.init_process_group(backend="gloo")
+    need = {0: [5, 60, 61], 1: [100, 7, 8, 9]}[rank]     # rank 0 alone would switch earlier than rank 1
+    s = MockSolver(need, tail_lanes=2, tail_chunk=16)
+    calls = []
+    red = gd.make_reduce_stats()
+
+    def reduce_stats(st):
+        calls.append(s.k)
+        return red(st)
+    newton_loop(s, 5000, reduce_stats=reduce_stats, sync_every=4)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, dict(events=s.events, calls=calls, n_iter=s.n_iter.numpy().tolist()))
+    if rank == 0:
+        import json
+        with open(out_path, "w") as f:
+            json.dump(gathered, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tail_switch_is_global_across_ranks(tmp_path):
+    """Two ranks with different local stragglers switch to the tail at the same iteration (the all-reduced active
+    count decides), issue the same collectives at the same iterations, and each ends with its lanes' counts."""
+    import json
+    out = str(tmp_path / "tail.json")
+    mp.start_processes(_tail_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    g = json.load(open(out))
+    t0 = [tuple(e) for e in g[0]["events"] if e[0] == "tail"]
+    t1 = [tuple(e) for e in g[1]["events"] if e[0] == "tail"]
+    # global active after k = 60: rank 0 {61} + rank 1 {100} = 2 -> both switch at 60 (rank 0 alone: at 8)
+    assert t0 == t1 and t0[0] == ("tail", 60, 76) and t0[-1][2] >= 100
+    assert g[0]["calls"] == g[1]["calls"]                 # paired collectives
+    assert g[0]["n_iter"] == [5, 60, 61] and g[1]["n_iter"] == [100, 7, 8, 9]
