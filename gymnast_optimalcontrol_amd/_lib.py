@@ -61,9 +61,12 @@ class GymArmijo(C.Structure):
 _P = C.c_void_p
 
 
+TIMING_POOL = 512        # GYM_TIMING_POOL
+
+
 class GymTiming(C.Structure):
     _fields_ = [("ev", _P * 20), ("ms", C.c_double * 10), ("launches", C.c_int64 * 10), ("pending", C.c_int32),
-                ("pad", C.c_int32)]
+                ("pool_used", C.c_int32), ("pool_ev", _P * (2 * TIMING_POOL)), ("pool_kind", C.c_int32 * TIMING_POOL)]
 
 
 class GymBatch(C.Structure):

@@ -2765,17 +2765,26 @@ __global__ __launch_bounds__(BLK) void k_fill_states(Dyn m, double2* __restrict_
     }
 }
 
-struct TimedLaunch {  // records a start/stop event pair around one launch if the slot is free
+struct TimedLaunch {  // records a start/stop event pair around one launch: a pool pair, else the kind's free slot
     gym_timing* t;
     int kind;
     hipStream_t s;
-    bool on;
-    TimedLaunch(gym_timing* t_, int kind_, hipStream_t s_)
-        : t(t_), kind(kind_), s(s_), on(t_ && !(t_->pending & (1 << kind_))) {
-        if (on) (void)hipEventRecord((hipEvent_t)t->ev[2 * kind], s);
+    int slot;            // pool index, -1: the kind's sampled pair, -2: not timed
+    TimedLaunch(gym_timing* t_, int kind_, hipStream_t s_) : t(t_), kind(kind_), s(s_), slot(-2) {
+        if (!t) return;
+        if (t->pool_used < GYM_TIMING_POOL && t->pool_ev[0]) {
+            slot = t->pool_used++;
+            t->pool_kind[slot] = kind;
+            (void)hipEventRecord((hipEvent_t)t->pool_ev[2 * slot], s);
+        } else if (!(t->pending & (1 << kind))) {
+            slot = -1;
+            (void)hipEventRecord((hipEvent_t)t->ev[2 * kind], s);
+        }
     }
     ~TimedLaunch() {
-        if (on) {
+        if (slot >= 0) {
+            (void)hipEventRecord((hipEvent_t)t->pool_ev[2 * slot + 1], s);
+        } else if (slot == -1) {
             (void)hipEventRecord((hipEvent_t)t->ev[2 * kind + 1], s);
             t->pending |= 1 << kind;
         }
@@ -3316,8 +3325,15 @@ int gym_timing_create(gym_timing* t) {
         if (r != hipSuccess) return (int)r;
         t->ev[i] = (void*)e;
     }
+    for (int i = 0; i < 2 * GYM_TIMING_POOL; ++i) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return (int)r;
+        t->pool_ev[i] = (void*)e;
+    }
     for (int i = 0; i < GYM_NK; ++i) { t->ms[i] = 0.0; t->launches[i] = 0; }
     t->pending = 0;
+    t->pool_used = 0;
     return 0;
 }
 
@@ -3325,6 +3341,9 @@ int gym_timing_destroy(gym_timing* t) {
     if (!t) return GYM_EINVAL;
     for (int i = 0; i < 2 * GYM_NK; ++i)
         if (t->ev[i]) { (void)hipEventDestroy((hipEvent_t)t->ev[i]); t->ev[i] = nullptr; }
+    for (int i = 0; i < 2 * GYM_TIMING_POOL; ++i)
+        if (t->pool_ev[i]) { (void)hipEventDestroy((hipEvent_t)t->pool_ev[i]); t->pool_ev[i] = nullptr; }
+    t->pool_used = 0;
     return 0;
 }
 
@@ -3339,6 +3358,14 @@ int gym_timing_collect(gym_timing* t) {
         t->launches[i] += 1;
     }
     t->pending = 0;
+    for (int j = 0; j < t->pool_used; ++j) {
+        float ms = 0.f;
+        hipError_t r = hipEventElapsedTime(&ms, (hipEvent_t)t->pool_ev[2 * j], (hipEvent_t)t->pool_ev[2 * j + 1]);
+        if (r != hipSuccess) return (int)r;
+        t->ms[t->pool_kind[j]] += ms;
+        t->launches[t->pool_kind[j]] += 1;
+    }
+    t->pool_used = 0;
     return 0;
 }
 

@@ -242,6 +242,7 @@ class BatchedNewtonSolver:
     def reset_timing(self):
         self.launches = {"phase": 0, "run": 0, "tail": 0, "iteration": 0}
         if self.timing is not None:
+            self.collect_timing()       # drains the pool (pairs of launches before the reset)
             for i in range(len(_lib.KERNEL_KINDS)):
                 self.timing.ms[i] = 0.0
                 self.timing.launches[i] = 0

@@ -101,15 +101,19 @@ typedef struct gym_armijo {
 /* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
  * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
  * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p), 7 sigma1 re-run of the lanes that
- * backtrack, 8 persistent run (gym_newton_run), 9 straggler tail (gym_newton_tail).  A pair is recorded only
- * if the previous one of its kind was collected. */
+ * backtrack, 8 persistent run (gym_newton_run), 9 straggler tail (gym_newton_tail).  Every launch is timed
+ * while the pool has room (gym_timing_collect empties it; the solvers collect at every host synchronisation);
+ * beyond that, a launch is timed only if the previous sampled pair of its kind was collected. */
 #define GYM_NK 10
+#define GYM_TIMING_POOL 512  /* event pairs for EVERY launch between two collects (then one sampled pair per kind) */
 typedef struct gym_timing {
     void* ev[2 * GYM_NK];    /* hipEvent_t start/stop pairs (gym_timing_create)          */
     double ms[GYM_NK];       /* accumulated device time per kernel kind                   */
     int64_t launches[GYM_NK];/* collected launches per kernel kind                        */
     int32_t pending;         /* bitmask: pairs recorded but not yet collected            */
-    int32_t pad;
+    int32_t pool_used;       /* pool pairs recorded since the last collect               */
+    void* pool_ev[2 * GYM_TIMING_POOL];  /* hipEvent_t pairs: every timed launch while the pool has room */
+    int32_t pool_kind[GYM_TIMING_POOL];  /* the kernel kind of each pool pair                          */
 } gym_timing;
 
 /* Device state of a batched solve (all device pointers, sizes in lanes / knots). */

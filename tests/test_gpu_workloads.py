@@ -314,3 +314,23 @@ def test_bench_spawns_ranks_on_the_gpu():
     for k in ("lane0_iters", "lane0_rel_l2_x", "lane_iters_min_max"):
         assert two["parity"][k] == one["parity"][k], k
     assert two["value"] > 0 and two["scaling"] == "weak"
+
+
+def test_kernel_timing_covers_every_launch():
+    """bench.py's roofline divides the algorithmic bytes by the phase kernel's average HIP-event time: every launch
+    between two host synchronisations is timed (GYM_TIMING_POOL), not a sample, on the pipelined and the persistent
+    schedules."""
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    x_ref, u_ref = load_refs()
+    eng = AcrobotEngine()
+    for kw, kinds, key in ((dict(pipeline=True), ("phase_odd", "phase_even"), "phase"),
+                           (dict(persistent=True, chunk=16), ("run",), "run")):
+        s = BatchedNewtonSolver(eng, x_ref, u_ref, 4096, tol=1e-4, gamma_0=0.1, **kw).enable_timing()
+        s.solve(make_x0(4096), 60, sync_every=4)
+        s.reset_timing()
+        s.solve(make_x0(4096), 60, sync_every=4)
+        kt = s.kernel_times()
+        assert sum(kt[k][1] for k in kinds) == s.launches[key] > 0, (kt, s.launches)
+        assert all(kt[k][0] > 0 for k in kinds)
