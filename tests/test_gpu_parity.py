@@ -209,7 +209,7 @@ def test_lane_independence_large_batch(golden, task2_refs):
     for j, i in enumerate(idx):
         assert n_iter[i] == L["n_iter"][j]
         assert rel_l2(r.x[i].cpu().numpy(), L["x"][j]) < TOL_TRAJ
-    sample = rng.choice(np.setdiff1d(np.arange(B), idx), 48, replace=False)
+    sample = rng.choice(np.setdiff1d(np.arange(B), idx), 1024, replace=False)   # ~3 s of the C oracle
     o = c_oracle.newton_solve(x0[sample], xr, ur, max_iters=5000, tol=1e-4, gamma_0=0.1)
     np.testing.assert_array_equal(n_iter[sample], o["n_iter"])
     np.testing.assert_array_equal(r.status.cpu().numpy()[sample], o["status"])
@@ -372,7 +372,8 @@ def test_u_ref_trim_and_errors(tg, task2_refs):
 @pytest.mark.parametrize("persistent", [False, True])
 def test_full_size_properties(task2_refs, persistent):
     """BASELINE cfg 3 size (262,144 lanes): the golden lane 0 within 1e-8, every headline lane converges
-    in the reference's iteration band, stats are consistent."""
+    in the reference's iteration band, stats are consistent, and 1,024 lanes spread over the batch match the C
+    oracle's decisions exactly and its trajectories within 1e-8."""
     from gymnast_optimalcontrol_amd import _lib
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
@@ -392,6 +393,15 @@ def test_full_size_properties(task2_refs, persistent):
         assert r.lane_iterations == int(sum(s[3] for s in r.stats_log))
     else:
         assert r.stats_log[-1][0] == 0 and r.stats_log[-1][5] == B
+    from oracle import c_oracle
+    pick = np.linspace(0, B - 1, 1024).astype(np.int64)
+    o = c_oracle.newton_solve(x0[pick], xr, ur, max_iters=5000, tol=1e-4, gamma_0=0.1)
+    np.testing.assert_array_equal(n[pick], o["n_iter"])
+    np.testing.assert_array_equal(r.n_rollouts.cpu().numpy()[pick], o["n_rollouts"])
+    xs, us = r.x[pick].cpu().numpy(), r.u[pick].cpu().numpy()
+    ex = np.linalg.norm((xs - o["x"]).reshape(1024, -1), axis=1) / np.linalg.norm(o["x"].reshape(1024, -1), axis=1)
+    eu = np.linalg.norm((us - o["u"]).reshape(1024, -1), axis=1) / np.linalg.norm(o["u"].reshape(1024, -1), axis=1)
+    assert ex.max() < TOL_TRAJ and eu.max() < TOL_TRAJ, (ex.max(), eu.max())
 
 
 @pytest.mark.parametrize("max_iters", [25, 5000])

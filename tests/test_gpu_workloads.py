@@ -78,7 +78,7 @@ def test_cfg4_global_batch_on_one_gpu():
     ni = r.n_iter.cpu().numpy()
     head = {k: getattr(r, k)[:4096].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")}
     head["n_iter"], head["n_roll"] = ni[:4096], r.n_rollouts[:4096].cpu().numpy()
-    pick = np.linspace(0, B - 1, 64).astype(np.int64)
+    pick = np.linspace(0, B - 1, 1024).astype(np.int64)   # ~3 s of the C oracle on the box's host cores
     xs, us = r.x[pick].cpu().numpy(), r.u[pick].cpu().numpy()
     x0l, u0l = r.x[0].cpu().numpy(), r.u[0].cpu().numpy()
     del r, s
