@@ -2765,6 +2765,13 @@ __global__ __launch_bounds__(BLK) void k_fill_states(Dyn m, double2* __restrict_
     }
 }
 
+// The kinds timed at every launch (pool pairs): the solver's main kernels (sweep, trial, phase, run, tail), whose
+// average duration is the roofline's denominator.  The short post-trial kernels (candidates, retry, statistics,
+// sigma1 re-run: five per phase) keep one sampled pair per kind and collect: an event pair around each of them
+// lengthened the phase-to-phase gap from ~28 to ~73 us in the rocprofv3 trace (+1-2% per solve).
+#ifndef GYM_TIMING_POOL_KINDS
+#define GYM_TIMING_POOL_KINDS ((1 << 0) | (1 << 1) | (1 << 5) | (1 << 6) | (1 << 8) | (1 << 9))
+#endif
 struct TimedLaunch {  // records a start/stop event pair around one launch: a pool pair, else the kind's free slot
     gym_timing* t;
     int kind;
@@ -2772,7 +2779,7 @@ struct TimedLaunch {  // records a start/stop event pair around one launch: a po
     int slot;            // pool index, -1: the kind's sampled pair, -2: not timed
     TimedLaunch(gym_timing* t_, int kind_, hipStream_t s_) : t(t_), kind(kind_), s(s_), slot(-2) {
         if (!t) return;
-        if (t->pool_used < GYM_TIMING_POOL && t->pool_ev[0]) {
+        if (((GYM_TIMING_POOL_KINDS >> kind) & 1) && t->pool_used < GYM_TIMING_POOL && t->pool_ev[0]) {
             slot = t->pool_used++;
             t->pool_kind[slot] = kind;
             (void)hipEventRecord((hipEvent_t)t->pool_ev[2 * slot], s);

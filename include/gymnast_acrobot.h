@@ -101,9 +101,10 @@ typedef struct gym_armijo {
 /* Optional per-kernel timing of gym_newton_iteration / gym_newton_phase with HIP events on the solver's
  * stream.  Kernel kinds: 0 backward sweep, 1 Armijo trial 1, 2 candidate trials, 3 accepted-candidate
  * rollout, 4 statistics, 5 / 6 fused pipeline phase (odd / even p), 7 sigma1 re-run of the lanes that
- * backtrack, 8 persistent run (gym_newton_run), 9 straggler tail (gym_newton_tail).  Every launch is timed
- * while the pool has room (gym_timing_collect empties it; the solvers collect at every host synchronisation);
- * beyond that, a launch is timed only if the previous sampled pair of its kind was collected. */
+ * backtrack, 8 persistent run (gym_newton_run), 9 straggler tail (gym_newton_tail).  Every launch of kinds
+ * 0, 1, 5, 6, 8, 9 is timed while the pool has room (gym_timing_collect empties it; the solvers collect at every
+ * host synchronisation); beyond that, and always for kinds 2, 3, 4, 7 (the short post-trial launches), a launch
+ * is timed only if the previous sampled pair of its kind was collected. */
 #define GYM_NK 10
 #define GYM_TIMING_POOL 512  /* event pairs for EVERY launch between two collects (then one sampled pair per kind) */
 typedef struct gym_timing {

@@ -2,14 +2,16 @@
 """Interleaved A/B timing of library variants in ONE process on one device (measurement tool).
 
     python tools/ab_bench.py --batch 262144 --rounds 3 lib_a.so lib_b.so:serial lib_b.so:pipe:nou0z ...
-(":serial" / ":pipe" / ":run" (persistent) select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":nock" the state
-checkpointing, ":noreorder" the Morton-order lane grouping of solve(); default:
+(":serial" / ":pipe" / ":run" (persistent) select the schedule, ":nou0z" disables the tau1 = 0 stream skipping, ":ck" enables the
+state checkpointing (the solver's default is off), ":noreorder" the Morton-order lane grouping of
+solve(), ":notime" the HIP-event kernel timing; default:
 the solver's choice)
 Each round runs one full batched solve per variant on the SAME device buffers (one solver whose
 kernel library is swapped), so buffer placement -- worth +-4% on its own -- is held fixed; prints
 per-variant median backward / trial kernel times and whole-solve throughput.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--max-iters", type=int, default=5000)
     ap.add_argument("--spread", type=float, default=0.5, help="th0 ~ U(+-spread) (1.5: the stress workload)")
+    ap.add_argument("--sync-every", type=int, default=4, help="host synchronisation cadence (bench.py's default)")
     a = ap.parse_args()
     import torch
     from bench import load_refs, make_x0
@@ -39,7 +42,7 @@ def main():
         path, *opts = spec.split(":")
         sched = {"serial": False, "pipe": True, "run": "run"}
         return (os.path.abspath(path), next((sched[o] for o in opts if o in sched), None), "nou0z" not in opts,
-                "nock" not in opts, "noreorder" not in opts)
+                "ck" in opts, "noreorder" not in opts, "notime" in opts)
     eng = AcrobotEngine(lib_path=split(a.libs[0])[0])
     s = BatchedNewtonSolver(eng, x_ref, u_ref, a.batch, tol=1e-4, gamma_0=0.1).enable_timing()
     default_pipe = s.pipeline
@@ -50,7 +53,7 @@ def main():
     for r in range(a.rounds + 1):
         for p in a.libs:
             eng.lib = libs[p]
-            _, sched, u0z, ck, reorder = split(p)
+            _, sched, u0z, ck, reorder, notime = split(p)
             s.reorder = reorder
             s.persistent = sched == "run"
             s.pipeline = default_pipe if sched in (None, "run") else sched
@@ -58,11 +61,17 @@ def main():
             s.checkpoint = ck and not s.persistent
             s.batch.flags = (_lib.FLAG_U0_ZERO if s.u0_zero else 0) | (_lib.FLAG_X_CKPT if s.checkpoint else 0)
             s.reset_timing()
-            out = s.solve(xd, a.max_iters)
+            s.batch.timing = None if notime else C.pointer(s.timing)
+            out = s.solve(xd, a.max_iters, sync_every=a.sync_every)
             kt = s.kernel_times()
+            if notime:
+                kt = {k: (0.0, 0) for k in kt}
             if r == 0:
                 continue   # warm-up round
-            if kt["run"][1]:     # persistent: the run launch(es) as "bwd", nothing as "trial"
+            if notime:
+                res[p]["bwd"].append(0.0)
+                res[p]["trial"].append(0.0)
+            elif kt["run"][1]:     # persistent: the run launch(es) as "bwd", nothing as "trial"
                 res[p]["bwd"].append(kt["run"][0] / kt["run"][1])
                 res[p]["trial"].append(0.0)
             elif kt["backward"][1]:
