@@ -431,47 +431,39 @@ struct Sweep {
                                            double& k1, double& k2, double& k3, double& s0, double& s1) {
         step_lin<U0Z>(w, stage_lin<U0Z>(m, w, J, xa, xb, ut0, ut1, xrt, urt), k0, k1, k2, k3, s0, s1);
     }
-    // the Riccati update of stage t from its linearisation (stage_lin: a function of x_t, u_t only)
+    // the Riccati update of stage t from its linearisation (stage_lin: a function of x_t, u_t only): the matrix half
+    // (gain row 1, P) and then the vector half (sigma, dJ, p, ||sigma||_inf)
     template <bool U0Z = false>
     __device__ __forceinline__ void step_lin(const KW& w, const Lin& L, double& k0, double& k1, double& k2,
                                              double& k3, double& s0, double& s1) {
-        // FMA contraction within each expression only, never across statements: the bits then do not depend on
-        // the context the stage is compiled into (the interleaved sweep of backward_solver_lane_ilp, the sigma1
-        // re-runs, the two-wavefront sweep of k_nt_run2) -- with cross-statement fusion they did
+        double G11, iG;
+        step_P(w, L, k0, k1, k2, k3, G11, iG);
+        step_p<U0Z>(w, L, k0, k1, k2, k3, G11, iG, s0, s1);
+    }
+    // The matrix half of step_lin: gain row 1 k = -(P b)^T A_d / G11, G11 = 2R1 + b^T P b and its reciprocal, and
+    // P <- 2Q + A_d^T P A_d - G11 k k^T.  A function of P and the stage's A_d, b only (not of p), so k_nt_run2
+    // runs it alone on its main wavefront and hands k, G11, 1/G11 to another wavefront for the vector half.
+    // FMA contraction within each expression only, never across statements: the bits then do not depend on the
+    // context the stage is compiled into (the interleaved sweep of backward_solver_lane_ilp, the sigma1 re-runs,
+    // the split sweep of k_nt_run2) -- with cross-statement fusion they did
+    __device__ __forceinline__ void step_P(const KW& w, const Lin& L, double& k0, double& k1, double& k2, double& k3,
+                                           double& G11, double& iG) {
 #pragma clang fp contract(on)
         const double dt = L.dt;
         const double A20 = L.A20, A21 = L.A21, A22 = L.A22, A23 = L.A23;
         const double A30 = L.A30, A31 = L.A31, A32 = L.A32, A33 = L.A33;
         const double bd2 = L.bd2, bd3 = L.bd3;
-        const double q0 = L.q0, q1 = L.q1, q2 = L.q2, q3 = L.q3, r0 = L.r0, r1 = L.r1;
-        if (LAMBDA) {  // lambda_t = 2Q dx_t + A_d^T lambda_{t+1}
-            const double n0 = q0 + (l0 + A20 * l2 + A30 * l3);
-            const double n1 = q1 + (l1 + A21 * l2 + A31 * l3);
-            const double n2 = q2 + (dt * l0 + A22 * l2 + A32 * l3);
-            const double n3 = q3 + (dt * l1 + A23 * l2 + A33 * l3);
-            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
-        }
         // Pb = P B_d[:,1]
         const double Pb0 = P02 * bd2 + P03 * bd3, Pb1 = P12 * bd2 + P13 * bd3;
         const double Pb2 = P22 * bd2 + P23 * bd3, Pb3 = P23 * bd2 + P33 * bd3;
-        const double G11 = w.twoR1 + (bd2 * Pb2 + bd3 * Pb3);
+        G11 = w.twoR1 + (bd2 * Pb2 + bd3 * Pb3);
         // F row 1 = (P b)^T A_d
         const double F0 = Pb0 + A20 * Pb2 + A30 * Pb3;
         const double F1 = Pb1 + A21 * Pb2 + A31 * Pb3;
         const double F2 = dt * Pb0 + A22 * Pb2 + A32 * Pb3;
         const double F3 = dt * Pb1 + A23 * Pb2 + A33 * Pb3;
-        const double g1 = r1 + (bd2 * p2 + bd3 * p3);
-        const double iG = gym::recip(G11);   // G11 = 2 R1 + b^T P b >= 2 R1 > 0: rcp + two Newton steps
+        iG = gym::recip(G11);   // G11 = 2 R1 + b^T P b >= 2 R1 > 0: rcp + two Newton steps
         k0 = -F0 * iG; k1 = -F1 * iG; k2 = -F2 * iG; k3 = -F3 * iG;
-        s1 = -g1 * iG;
-        if (U0Z) {   // r0 = +0: sigma0 = -0, and r0 sigma0 + g1 sigma1 = g1 sigma1 exactly
-            s0 = -0.0;
-            const double d1 = g1 * s1;
-            dJ += d1;
-        } else {
-            s0 = -r0 * w.iG00;
-            dJ += r0 * s0 + g1 * s1;
-        }
         // W = P A_d
         const double W00 = P00 + P02 * A20 + P03 * A30, W01 = P01 + P02 * A21 + P03 * A31;
         const double W02 = dt * P00 + P02 * A22 + P03 * A32, W03 = dt * P01 + P02 * A23 + P03 * A33;
@@ -493,14 +485,43 @@ struct Sweep {
         const double nP22 = w.twoQ[2] + (dt * W02 + A22 * W22 + A32 * W32) - gk2 * k2;
         const double nP23 = (dt * W03 + A22 * W23 + A32 * W33) - gk2 * k3;
         const double nP33 = w.twoQ[3] + (dt * W13 + A23 * W23 + A33 * W33) - gk3 * k3;
+        P00 = nP00; P01 = nP01; P02 = nP02; P03 = nP03; P11 = nP11; P12 = nP12; P13 = nP13;
+        P22 = nP22; P23 = nP23; P33 = nP33;
+    }
+    // The vector half of step_lin from the stage's gain row, G11 and 1/G11 (step_P): the costate (LAMBDA), sigma,
+    // dJ, p <- q + A_d^T p - K^T G sigma and the running ||sigma||_inf.  Not a function of P.
+    template <bool U0Z = false>
+    __device__ __forceinline__ void step_p(const KW& w, const Lin& L, double k0, double k1, double k2, double k3,
+                                           double G11, double iG, double& s0, double& s1) {
+#pragma clang fp contract(on)
+        const double dt = L.dt;
+        const double A20 = L.A20, A21 = L.A21, A22 = L.A22, A23 = L.A23;
+        const double A30 = L.A30, A31 = L.A31, A32 = L.A32, A33 = L.A33;
+        const double bd2 = L.bd2, bd3 = L.bd3;
+        const double q0 = L.q0, q1 = L.q1, q2 = L.q2, q3 = L.q3, r0 = L.r0, r1 = L.r1;
+        if (LAMBDA) {  // lambda_t = 2Q dx_t + A_d^T lambda_{t+1}
+            const double n0 = q0 + (l0 + A20 * l2 + A30 * l3);
+            const double n1 = q1 + (l1 + A21 * l2 + A31 * l3);
+            const double n2 = q2 + (dt * l0 + A22 * l2 + A32 * l3);
+            const double n3 = q3 + (dt * l1 + A23 * l2 + A33 * l3);
+            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
+        }
+        const double g1 = r1 + (bd2 * p2 + bd3 * p3);
+        s1 = -g1 * iG;
+        if (U0Z) {   // r0 = +0: sigma0 = -0, and r0 sigma0 + g1 sigma1 = g1 sigma1 exactly
+            s0 = -0.0;
+            const double d1 = g1 * s1;
+            dJ += d1;
+        } else {
+            s0 = -r0 * w.iG00;
+            dJ += r0 * s0 + g1 * s1;
+        }
         // p <- q + A_d^T p - K^T G sigma
         const double gs = G11 * s1;
         const double np0 = q0 + (p0 + A20 * p2 + A30 * p3) - k0 * gs;
         const double np1 = q1 + (p1 + A21 * p2 + A31 * p3) - k1 * gs;
         const double np2 = q2 + (dt * p0 + A22 * p2 + A32 * p3) - k2 * gs;
         const double np3 = q3 + (dt * p1 + A23 * p2 + A33 * p3) - k3 * gs;
-        P00 = nP00; P01 = nP01; P02 = nP02; P03 = nP03; P11 = nP11; P12 = nP12; P13 = nP13;
-        P22 = nP22; P23 = nP23; P33 = nP33;
         p0 = np0; p1 = np1; p2 = np2; p3 = np3;
         // U0Z: |sigma0| = 0 never raises smax (>= 0 or NaN)
         smax = U0Z ? gym::nanmax_abs(smax, s1) : gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
@@ -1827,8 +1848,22 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
 #define GYM_RUN2_C 2
 #endif
 constexpr int R2C = GYM_RUN2_C;   // stages per chunk (even)
-constexpr int R2S = 2 * R2C;      // ring slots
+constexpr int R2S = 3 * R2C;      // ring slots (the trial uses two chunks of them, the split sweep three)
 constexpr int R2W = 11;           // pairs per lane and slot: sweep x_t (2), u_t, Lin (8); trial x_{t+1} (2), u1_t
+#ifndef GYM_RUN2_PAIR
+#define GYM_RUN2_PAIR 1
+#endif
+#ifndef GYM_RUN2_SPLIT
+#define GYM_RUN2_SPLIT 1
+#endif
+// GYM_RUN2_SPLIT (with the lane-pair wavefront, GYM_RUN2_PAIR): the sweep's Riccati update is split over two
+// wavefronts, the main one running only the matrix half (Sweep::step_P: gain row, P) and handing k, G11, 1/G11 to
+// the pair wavefront, which runs the vector half (step_p: sigma, dJ, p, ||sigma||) and the K1 / cg stores one chunk
+// behind.  Nothing flows back, so the main wavefront's chain loses the vector half, the stores and 6 of its 11
+// ring reads per stage.  The helpers' ring is then three chunks deep (the pair wavefront reads chunk c - 1 while
+// the main one reads c and the helpers write c + 1).
+constexpr bool R2SPLIT = GYM_RUN2_SPLIT && GYM_RUN2_PAIR;
+constexpr int R2RD = R2SPLIT ? 3 : 2;   // helper ring depth in chunks (sweep)
 #ifndef GYM_RUN2_PD
 #define GYM_RUN2_PD 4
 #endif
@@ -1944,12 +1979,13 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
                 SweepStage w = P[set];
                 in_vgpr2(w.xa); in_vgpr2(w.xb); gym::in_vgpr(w.u0); gym::in_vgpr(w.u1);
                 fetch(P[set], uni(max(T - 1 - (i + R2PD), 0)));
-                produce(w, uni(max(T - 1 - i, 0)), (c & 1) * R2C + j);   // past the end: not consumed
+                produce(w, uni(max(T - 1 - i, 0)), (c % R2RD) * R2C + j);   // past the end: not consumed
             }
             lds_barrier(bw);
         }
     }
     lds_barrier(bw);
+    if (R2SPLIT) lds_barrier(bw);          // the vector half's last chunk
 }
 
 // main wavefront, sweep: the Riccati recursion from the ring; K row 1 / cg stored for active lanes
@@ -1973,7 +2009,7 @@ __device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l
         for (int j = 0; j < R2C; ++j) {
             const int i = c * R2C + j;
             if (i < T) {
-                const double2(*s)[BLK] = ring[(c & 1) * R2C + j];
+                const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
                 const double2 xa = s[0][lane], xb = s[1][lane], uu = s[2][lane];
                 const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
                 const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
@@ -1984,6 +2020,88 @@ __device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l
                 S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
                 if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, k0, k1, k2,
                                                  k3, s1);
+            }
+        }
+        lds_barrier(bw);
+    }
+    dJ_out = S.dJ;
+    smax_out = S.smax;
+}
+
+// GYM_RUN2_SPLIT, main wavefront, sweep: the matrix half of the Riccati recursion (Sweep::step_P) from the ring's
+// A_d rows and b; stage i's gain row, G11 and 1/G11 into the gain ring (slot (c & 1) * R2C + j) for the pair
+// wavefront.  Chunk c between barriers c and c + 1, as run2_sweep_main.
+typedef double2 (*gring_t)[3][BLK];
+template <bool U0Z, bool RL>
+__device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int lane, int64_t l, int cb,
+                                                unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const double2* x = R->x[cb];
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, R->Bp)], x[wix(T, 1, 2, l, R->Bp)], run_xr<RL>(R, l) + 4 * T);
+    const int nch = run2_chunks(T);
+    lds_barrier(bw);                       // the helpers' chunk 0
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            const int i = c * R2C + j;
+            if (i < T) {
+                const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
+                const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
+                const double2 bd = s[7][lane];
+                const KArgs ka = kernarg_consts();
+                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
+                            0.0, 0.0, 0.0, 0.0, 0.0, 0.0, ka.m.h};   // q, r: the vector half's
+                double k0, k1, k2, k3, G11, iG;
+                S.step_P(ka.w, L, k0, k1, k2, k3, G11, iG);
+                double2(*g)[BLK] = gring[(c & 1) * R2C + j];
+                g[0][lane] = make_double2(k0, k1);
+                g[1][lane] = make_double2(k2, k3);
+                g[2][lane] = make_double2(G11, iG);
+            }
+        }
+        lds_barrier(bw);
+    }
+    lds_barrier(bw);                       // the vector half's last chunk
+}
+
+// GYM_RUN2_SPLIT, pair wavefront, sweep: the vector half (Sweep::step_p) of stage i from the helpers' ring (chunk
+// c, still in its slot: three chunks deep) and the main wavefront's gain ring; K row 1 / cg stored for active lanes.
+// Chunk c between barriers c + 1 and c + 2.
+template <bool U0Z, bool RL>
+__device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int lane, int64_t l, int cb, bool act,
+                                               double& dJ_out, double& smax_out, unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double g0 = R->a.gamma0;
+    const double2* x = R->x[cb];
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], run_xr<RL>(R, l) + 4 * T);
+    const int nch = run2_chunks(T);
+    lds_barrier(bw);                       // the helpers' chunk 0
+    lds_barrier(bw);                       // the main wavefront's chunk 0
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            const int i = c * R2C + j;
+            if (i < T) {
+                const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
+                const double2 xa = s[0][lane], xb = s[1][lane], uu = s[2][lane];
+                const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
+                const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
+                const double2(*g)[BLK] = gring[(c & 1) * R2C + j];
+                const double2 ka01 = g[0][lane], ka23 = g[1][lane], gi = g[2][lane];
+                const KArgs ka = kernarg_consts();
+                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
+                            qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
+                double s0, s1;
+                S.step_p<U0Z>(ka.w, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
+                if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
+                                                 ka01.y, ka23.x, ka23.y, s1);
             }
         }
         lds_barrier(bw);
@@ -2164,9 +2282,6 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
 #endif
 constexpr int R2H = GYM_RUN2_HELPERS;   // helper wavefronts: the sweep's stages are dealt to them round-robin
 static_assert(R2H == 1 || R2H == 2, "one or two helper wavefronts");
-#ifndef GYM_RUN2_PAIR
-#define GYM_RUN2_PAIR 1
-#endif
 // GYM_RUN2_PAIR: a further wavefront (index R2H + 1) joins the main one in the trial, each trajectory's RK4 chain
 // on a lane pair (run2_trial_main_pair); it idles through the sweep
 constexpr int R2P = GYM_RUN2_PAIR;
@@ -2181,6 +2296,7 @@ __device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
 template <bool U0Z, bool RL>
 __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
     __shared__ double2 ring[R2S][R2W][BLK];
+    __shared__ double2 gring[R2SPLIT ? 2 * R2C : 1][3][BLK];   // GYM_RUN2_SPLIT: gain rows, G11, 1/G11
     __shared__ double shJ[BLK];
     __shared__ int shst[BLK];
     const int lane = threadIdx.x & (BLK - 1);
@@ -2202,11 +2318,16 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
         } else if (wave == 2 && R2H == 2) {
             run2_sweep_helper<U0Z, R2H - 1, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l),
                                                      run_ur<RL>(run_args(), l), acc[4]);
-        } else if (wave > R2H) {
+        } else if (wave > R2H && !R2SPLIT) {
             run2_idle(run_args()->N - 1, acc[4]);
-        } else {
+        } else if (wave == 0 && R2SPLIT) {
+            run2_sweep_gain<U0Z, RL>(ring, gring, lane, l, cb, acc[4]);
+        } else {   // the main wavefront, or with GYM_RUN2_SPLIT the pair wavefront (the vector half, the stores)
             double d, s;
-            run2_sweep_main<U0Z, RL>(ring, lane, l, cb, act, d, s, acc[4]);
+            if (R2SPLIT)
+                run2_sweep_vec<U0Z, RL>(ring, gring, lane, l, cb, act, d, s, acc[4]);
+            else
+                run2_sweep_main<U0Z, RL>(ring, lane, l, cb, act, d, s, acc[4]);
             const rargs_t Q = run_args();
             if (act) {
                 Q->dJ[l] = d;
