@@ -2466,8 +2466,20 @@ __device__ __forceinline__ targs_t tail_args() {
 // the trial loop issues no global loads: its scratch stores are never waited on (the GFX9 vmcnt counts both)
 constexpr int TL_TST = 8;
 constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / exchange areas within 56 KiB of LDS
+#ifndef GYM_TAIL_SPLIT
+#define GYM_TAIL_SPLIT 1
+#endif
+// GYM_TAIL_SPLIT: two wavefronts per tail lane, the sweep's Riccati update split as in k_nt_run2 (Sweep::step_P on
+// wavefront 0, Sweep::step_p, the stores and the next pass's linearisations on wavefront 1, one 64-stage pass
+// behind; linearisations triple-buffered, the gain rows double-buffered); the trials stay on wavefront 0
+constexpr bool TL_SPLIT = GYM_TAIL_SPLIT && !GYM_TAIL_QUAD;
+constexpr int TL_THREADS = TL_SPLIT ? 2 * BLK : BLK;
+constexpr int TL_GK = 6;         // doubles per stage in the gain ring: k row 1 (4), G11, 1/G11
 constexpr size_t tail_lds_bytes(int T) {
-    return sizeof(double) * ((size_t)TL_STAGES * TL_PITCH + (size_t)(BLK / 4) * QX_DOUBLES + (size_t)T * TL_TST);
+    return TL_SPLIT ? sizeof(double) * ((size_t)3 * TL_STAGES * TL_PITCH + (size_t)2 * TL_STAGES * TL_GK + 4 +
+                                        (size_t)T * TL_TST)
+                    : sizeof(double) * ((size_t)TL_STAGES * TL_PITCH + (size_t)(BLK / 4) * QX_DOUBLES +
+                                        (size_t)T * TL_TST);
 }
 // the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage (global, and staged in tst); returns dJ,
 // max|sigma|
@@ -2539,6 +2551,106 @@ __device__ __forceinline__ void tail_sweep(double* lin, double* xq, double* tst,
     smax_out = GYM_TAIL_QUAD ? Q.smax : S.smax;
 }
 
+// GYM_TAIL_SPLIT: the sweep of lane l on two wavefronts.  Pass j covers stages T-1-64j down to T-64-64j.  Between
+// workgroup barriers j and j+1, wavefront 0 runs the matrix half over pass j (linearisations lin3[j % 3], gain rows
+// into gk2[j & 1]) while wavefront 1 runs the vector half over pass j - 1 (its linearisations and gain rows, K row
+// 1 / cg / sigma1 stored and staged in tst) and then evaluates pass j + 1's linearisations.  Every thread of a
+// wavefront runs the same recursion (the same bits); its lane 0 writes.  dJ and max|sigma| land in shd[0..1].
+template <bool U0Z, bool RL>
+__device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, double* shd, double* tst, int wave,
+                                                 int lane, int64_t l, int cb) {
+    const targs_t R = tail_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double2* x = R->x[cb];
+    const double* u = R->u[cb];
+    const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+    const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    const double g0 = R->a.gamma0;
+    const double dt = R->m.h;
+    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
+    const int np = (T + TL_STAGES - 1) / TL_STAGES;
+    auto linearise = [&](int j) {   // wavefront 1: pass j's linearisations, thread i stage T-1-64j-i
+        const int t = T - 1 - j * TL_STAGES - lane;
+        if (t >= 0) {
+            const double2 xa = x[wix(t, 0, 2, l, Bp)], xb = x[wix(t, 1, 2, l, Bp)];
+            const double u0 = U0Z ? 0.0 : u[pix(t, 0, 2, l, Bp)], u1 = u[pix(t, 1, 2, l, Bp)];
+            const KArgs ka = kernarg_consts();
+            const gym::Jac J = gym::jacobian(ka.m, xa.x, xa.y, xb.x, xb.y, u1);
+            const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, xa, xb, u0, u1, xr + 4 * t, ur + 2 * t);
+            double* s = lin3 + ((j % 3) * TL_STAGES + lane) * TL_PITCH;
+            s[0] = L.A20; s[1] = L.A21; s[2] = L.A22; s[3] = L.A23;
+            s[4] = L.A30; s[5] = L.A31; s[6] = L.A32; s[7] = L.A33;
+            s[8] = L.bd2; s[9] = L.bd3; s[10] = L.q0; s[11] = L.q1;
+            s[12] = L.q2; s[13] = L.q3; s[14] = L.r0; s[15] = L.r1;
+            s[16] = xa.x; s[17] = xa.y; s[18] = xb.x; s[19] = xb.y; s[20] = u1;
+            tst[t * TL_TST + 6] = u0;
+        }
+    };
+    if (wave == 1) linearise(0);
+    __syncthreads();
+    for (int j = 0; j <= np; ++j) {
+        if (wave == 0) {
+            if (j < np) {
+                const int tb = T - 1 - j * TL_STAGES;
+                const int n = tb + 1 < TL_STAGES ? tb + 1 : TL_STAGES;
+                const double* L3 = lin3 + (j % 3) * TL_STAGES * TL_PITCH;
+                double* G = gk2 + (j & 1) * TL_STAGES * TL_GK;
+                for (int i = 0; i < n; ++i) {
+                    const double* s = L3 + i * TL_PITCH;
+                    const KArgs ka = kernarg_consts();
+                    const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                                0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dt};   // q, r: the vector half's
+                    double k0, k1, k2, k3, G11, iG;
+                    S.step_P(ka.w, L, k0, k1, k2, k3, G11, iG);
+                    if (lane == 0) {
+                        double* g = G + i * TL_GK;
+                        g[0] = k0; g[1] = k1; g[2] = k2; g[3] = k3; g[4] = G11; g[5] = iG;
+                    }
+                }
+            }
+        } else {
+            if (j >= 1) {
+                const int jj = j - 1;
+                const int tb = T - 1 - jj * TL_STAGES;
+                const int n = tb + 1 < TL_STAGES ? tb + 1 : TL_STAGES;
+                const double* L3 = lin3 + (jj % 3) * TL_STAGES * TL_PITCH;
+                const double* G = gk2 + (jj & 1) * TL_STAGES * TL_GK;
+                for (int i = 0; i < n; ++i) {
+                    const double* s = L3 + i * TL_PITCH;
+                    const double* g = G + i * TL_GK;
+                    const double k0 = g[0], k1 = g[1], k2 = g[2], k3 = g[3];
+                    const KArgs ka = kernarg_consts();
+                    const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                                s[10], s[11], s[12], s[13], s[14], s[15], dt};
+                    double s0, s1;
+                    S.step_p<U0Z>(ka.w, L, k0, k1, k2, k3, g[4], g[5], s0, s1);
+                    if (lane == 0) {
+                        const int ts = tb - i;
+                        const double2 xa = make_double2(s[16], s[17]), xb = make_double2(s[18], s[19]);
+                        const double cg = stage_cg(xa, xb, s[20], g0, k0, k1, k2, k3, s1);
+                        double* q = tst + ts * TL_TST;
+                        q[0] = k0; q[1] = k1; q[2] = k2; q[3] = k3; q[4] = cg; q[5] = s1;
+                        const auto rC = rsrc(Cb + (int64_t)ts * row);
+                        const auto rK = rsrc(Kb + (int64_t)ts * (2 * (int64_t)row));
+                        bst2(rK, o2, 0, k0, k1);
+                        bst2(rK, o2, WROW, k2, k3);
+                        bst1(rC, o1, 0, cg);
+                        bst1(rC, o1, plane, s1);
+                    }
+                }
+            }
+            if (j + 1 < np) linearise(j + 1);
+            if (j == np && lane == 0) { shd[0] = S.dJ; shd[1] = S.smax; }
+        }
+        __syncthreads();
+    }
+}
+
 // Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) into virtual lane v of the
 // scratch, its streams from the staging tst; returns the candidate's cost
 template <bool U0Z, bool RL, bool PAIR>
@@ -2605,12 +2717,16 @@ __device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, i
 __device__ unsigned long long g_tail_trace[4096][4];
 #endif
 template <bool U0Z, bool RL, bool PAIR>
-__global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
+__global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
     extern __shared__ double tail_lds[];          // tail_lds_bytes(T): linearisations, quad exchange, trial staging
+    // TL_SPLIT: lin3 (3 passes) | gk2 (2 passes of gain rows) | shd (dJ, max|sigma|, the decision) | tst
     double* lin = tail_lds;
     double* xq = lin + TL_STAGES * TL_PITCH;
-    double* tst = xq + (BLK / 4) * QX_DOUBLES;
-    const int lane = threadIdx.x;
+    double* gk2 = lin + 3 * TL_STAGES * TL_PITCH;
+    double* shd = gk2 + 2 * TL_STAGES * TL_GK;
+    double* tst = TL_SPLIT ? shd + 4 : xq + (BLK / 4) * QX_DOUBLES;
+    const int lane = threadIdx.x & (BLK - 1);
+    const int wave = threadIdx.x / BLK;           // TL_SPLIT: 0 the matrix half and the trials, 1 the vector half
     const int64_t l = tail_args()->list[blockIdx.x];
     int st = tail_args()->status[l];
     unsigned long long acc[4] = {0, 0, 0, 0};   // GYM_TAIL_TRACE only
@@ -2619,12 +2735,18 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         double dJ, sm;
         unsigned long long tt = R2T_NOW();
         ++acc[3];
-        tail_sweep<U0Z, RL>(lin, xq, tst, lane, l, cb, dJ, sm);
+        if (TL_SPLIT) {
+            tail_sweep_split<U0Z, RL>(lin, gk2, shd, tst, wave, lane, l, cb);   // ends at a workgroup barrier
+            dJ = shd[0];
+            sm = shd[1];
+        } else {
+            tail_sweep<U0Z, RL>(lin, xq, tst, lane, l, cb, dJ, sm);
+        }
         acc[0] += R2T_NOW() - tt;
         tt = R2T_NOW();
         {
             const targs_t Q = tail_args();
-            if (lane == 0) {
+            if (lane == 0 && wave == 0) {
                 Q->dJ[l] = dJ;
                 Q->smax[l] = sm;
                 if (Q->hist_smax && k < Q->a.hist_len) Q->hist_smax[(int64_t)k * Q->Bp + l] = sm;
@@ -2638,7 +2760,7 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         for (int q = 0; q < cand && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
         bool ok = false;
         double Jn = 0.0;
-        if (cand < max_ls) {
+        if (cand < max_ls && wave == 0) {
             Jn = tail_candidate<U0Z, RL, PAIR>(tst, l, cb, cand, g, v, lane & 1);
             const targs_t R = tail_args();
             ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
@@ -2646,11 +2768,17 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         const unsigned long long okm = __ballot(ok);
         acc[1] += R2T_NOW() - tt;
         tt = R2T_NOW();
-        // the first accepted trial, in order (PAIR: both lanes of a pair hold the same decision)
-        const int first = okm ? (__ffsll((long long)okm) - 1) / (PAIR ? 2 : 1) : -1;
+        // the first accepted trial, in order (PAIR: both lanes of a pair hold the same decision); TL_SPLIT: wavefront
+        // 0's, handed to wavefront 1 so that both leave the iteration loop together
+        int first = okm ? (__ffsll((long long)okm) - 1) / (PAIR ? 2 : 1) : -1;
+        if (TL_SPLIT) {
+            if (wave == 0 && lane == 0) shd[2] = (double)first;
+            __syncthreads();
+            first = (int)shd[2];
+        }
         const int nr = first >= 0 ? first + 1 : max_ls;
         lane_fence();   // the candidates' scratch stores, before the copy reads them
-        if (first >= 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
+        if (first >= 0 && wave == 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
             const targs_t R = tail_args();
             const int T = R->N - 1;
             const int64_t vf = (int64_t)blockIdx.x * max_ls + first;
@@ -2686,7 +2814,7 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         const int src = (first >= 0 ? first : 0) * (PAIR ? 2 : 1);
         const double Jf = __shfl(Jn, src);
         const double gf = __shfl(g, src);
-        if (lane == 0) {
+        if (lane == 0 && wave == 0) {
             const targs_t F = tail_args();
             F->n_roll[l] += nr;
             F->n_iter[l] += 1;
@@ -2703,7 +2831,7 @@ __global__ __launch_bounds__(BLK, 1) void k_nt_tail(TailArgs args) {
         acc[2] += R2T_NOW() - tt;
     }
 #ifdef GYM_TAIL_TRACE
-    if (lane == 0 && blockIdx.x < 4096)
+    if (threadIdx.x == 0 && blockIdx.x < 4096)
         for (int i = 0; i < 4; ++i) g_tail_trace[blockIdx.x][i] += acc[i];
 #endif
 }
@@ -3329,7 +3457,13 @@ int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* 
                                      : (u0z ? k_nt_tail<true, false, true> : k_nt_tail<false, false, true>))
                                : (rl ? (u0z ? k_nt_tail<true, true, false> : k_nt_tail<false, true, false>)
                                      : (u0z ? k_nt_tail<true, false, false> : k_nt_tail<false, false, false>));
-        hipLaunchKernelGGL(kern, dim3((unsigned)n_lanes), dim3(BLK), tail_lds_bytes(b->N - 1), st, ta);
+        const size_t lds = tail_lds_bytes(b->N - 1);
+        if (lds > 65536) {   // above the default dynamic-LDS limit (gfx950: 160 KiB per workgroup)
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return (int)e;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)n_lanes), dim3(TL_THREADS), lds, st, ta);
     }
     // the statistics after iteration k1 - 1, over the whole batch (as gym_newton_run)
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
