@@ -379,6 +379,15 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
     }
 }
 
+// 16-B non-temporal store: the trajectories are written once and not read back by this kernel.  The per-step
+// stores land in rows 16 KB apart (the reference's lane-major arrays); streamed past the caches they cost the
+// latency-bound rollout less (cfg 5: 426 -> 412 us, tools/rollout_probe.py; staging the steps in LDS to write
+// whole-trajectory runs was slower, 458 us: LDS traffic shares lgkmcnt with the per-step scalar loads)
+__device__ __forceinline__ void st_nt2(double2* p, double a, double b) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(d2v{a, b}, reinterpret_cast<d2v*>(p));
+}
+
 // k_track_rollout with each trajectory on a lane pair (gym::rk4_pair): 2B threads, 128 B... of one lane's rows
 // split between the pair (even lane: (th1, th2) and u; odd lane: (w1, w2)).  The chain of 500 dependent RK4 steps
 // is the whole cost of this latency-bound kernel (B/32 wavefronts, one per SIMD), and the split shortens each
@@ -416,9 +425,10 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
             for (int q = 0; q < 4; ++q) r[q] = x_ff[4 * (t + 1) + q];
             f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
         }
-        if (!odd) ul[t] = make_double2(v0, v1);
+        if (!odd) st_nt2(ul + t, v0, v1);
         gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
-        xl[2 * (t + 1)] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+        if (odd) st_nt2(xl + 2 * (t + 1), n2, n3);
+        else st_nt2(xl + 2 * (t + 1), n0, n1);
     }
 }
 

@@ -99,3 +99,26 @@ def test_straggler_tail_on_the_automatic_schedule():
     r = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=0, **kw).solve(x0, 700)
     for f in FIELDS[:9]:
         _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f)
+
+
+@pytest.mark.parametrize("N", [2, 6, 65, 66, 130, 203])
+def test_straggler_tail_on_short_and_ragged_horizons(N):
+    """The tail's sweep works through the horizon in 64-stage passes (linearisations triple-buffered, the split
+    Riccati halves one pass apart): one-stage, single-pass, exactly-one-pass, one-past and multi-pass ragged
+    horizons, bit for bit the serial schedule."""
+    from bench import load_refs
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur = load_refs()
+    xr, ur = xr[:N].copy(), ur[:N - 1].copy()
+    B, max_iters = 130, 40
+    x0 = _hard_lanes(B, seed=11)
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, hist_len=max_iters)
+    r = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=0, **kw).solve(x0, max_iters)
+    s = BatchedNewtonSolver(eng, xr, ur, B, pipeline=False, tail_lanes=10 ** 9, **kw)
+    assert s.tail_lanes > 0
+    t = s.solve(x0, max_iters)
+    assert s.launches["tail"] > 0
+    for f in FIELDS:
+        _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"N={N}: {f}")
