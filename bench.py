@@ -201,7 +201,8 @@ class NewtonLeg:
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
             schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
-            split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes)
+            split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes,
+            compact=None if a.compact == "auto" else a.compact == "on")
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
@@ -217,17 +218,19 @@ class NewtonLeg:
         gd.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        lane_its, rolls, res, tail_its = 0, 0, None, 0
+        lane_its, rolls, res, tail_its, compactions = 0, 0, None, 0, 0
         for _ in range(steps):
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
             lane_its += res.lane_iterations
             rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
             tail_its += res.tail_lane_iterations
+            compactions += res.compactions
         torch.cuda.synchronize()
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
         self.res, self.lane_its, self.steps, self.tail_lane_its = res, lane_its, steps, tail_its
+        self.compactions = compactions
         self.elapsed = elapsed
         self.lane_its_all = int(gd.sum_over_ranks(lane_its))
         self.rollouts_all = int(gd.sum_over_ranks(rolls))
@@ -380,6 +383,9 @@ def main():
     ap.add_argument("--tail-lanes", type=int, default=None,
                     help="straggler tail: hand the last lanes to gym_newton_tail once at most this many are active "
                          "(default: the solver's, 4 per CU; 0 = off)")
+    ap.add_argument("--compact", choices=("auto", "on", "off"), default="auto",
+                    help="lane compaction of the serial / pipelined loop (BatchedNewtonSolver.maybe_compact; auto: "
+                         "the solver's default, on with the automatic schedule)")
     ap.add_argument("--split-waves", choices=("on", "off"), default="on",
                     help="persistent schedule: two wavefronts per 64 lanes (k_nt_run2, default) or one (k_nt_run)")
     ap.add_argument("--dry-run", action="store_true",
@@ -490,6 +496,10 @@ def main():
         "share_of_lane_iterations": main_leg.tail_lane_its / max(main_leg.lane_its, 1),
         "note": "gym_newton_tail: once at most lanes_threshold lanes are active (all ranks), one workgroup per lane, "
                 "every Armijo trial at once (bitwise the serial schedule, tests/test_gpu_tail.py)"}
+    out["lane_compaction"] = {
+        "enabled": bool(sv.compact_mode), "compactions_per_step": main_leg.compactions / max(a.steps, 1),
+        "note": "active lanes moved to the front of each launch range when few remain spread over many wavefronts "
+                "(BatchedNewtonSolver.maybe_compact; bitwise invisible, tests/test_gpu_tail.py)"}
 
     kern, roof = main_leg.kernel_report(N)
     if kern and rank == 0:

@@ -63,6 +63,7 @@ class SolveResult:
     sigmas: dict | None = None              # {lane: {iteration: sigma (T,2)}} of the captured lanes (capture_sigma)
     schedule: str = ""                      # "serial" | "pipelined" | "persistent"
     tail_lane_iterations: int = 0           # lane-iterations run by the straggler tail (gym_newton_tail)
+    compactions: int = 0                    # lane compactions during the loop (BatchedNewtonSolver.compact)
 
 
 class BatchedNewtonSolver:
@@ -98,7 +99,8 @@ class BatchedNewtonSolver:
                  u0_zero: bool | None = None, checkpoint: bool = False, persistent: bool | None = None,
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
                  capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
-                 capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128):
+                 capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128,
+                 compact: bool | None = None):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -220,6 +222,15 @@ class BatchedNewtonSolver:
                    engine.lib.gym_newton_tail_scratch(self.N, 1, int(max_ls), C.byref(need)) == 0)
         self.tail_lanes = int(tail_lanes) if tail_ok else 0
         self.tail_chunk = max(int(tail_chunk), 1)
+        # lane compaction (serial / pipelined schedules, solve(); see maybe_compact): default on with the automatic
+        # schedule choice.  "force" compacts at every host synchronisation (tests)
+        if compact is None:
+            compact = auto_schedule
+        self.compact_mode = ("force" if compact == "force" else bool(compact)) if (
+            not self.persistent and not self.checkpoint and self.capture_lanes is None) else False
+        self.compactions = 0
+        self._compact_prev = None
+        self.lane_order_live = False   # True inside solve(), whose results follow lane_order back
         self._tail_scratch = None
         self.tail_lane_its = 0
         self._cap_pos = None
@@ -455,6 +466,74 @@ class BatchedNewtonSolver:
                                                  self.eng.stream), "gym_newton_sigma")
         return s
 
+    # --- lane compaction ------------------------------------------------------------------
+    COMPACT_MAX_SHARE = 0.25   # consider compacting once at most this share of the lanes is active ...
+    COMPACT_MIN_KEEP = 0.5     # ... and the active count kept at least half its value since the last sync
+
+    def maybe_compact(self, active: int) -> bool:
+        """At a host synchronisation (iteration boundary): compact the lanes if few remain active but they are
+        spread over many wavefronts.  A wavefront runs its whole chains while any of its 64 lanes is active, so
+        late in a hard solve (SURVEY 8(d)'s stress batch: ~22,000 of 262,144 lanes active for hundreds of
+        iterations) every SIMD still runs its four wavefronts for a few lanes each.  ``active``: this rank's count.
+        The trigger is rank-local (compaction changes no collective)."""
+        if not self.compact_mode:
+            return False
+        prev, self._compact_prev = self._compact_prev, int(active)
+        if active <= 0:
+            return False
+        if self.compact_mode != "force":
+            if active > self.COMPACT_MAX_SHARE * self.B or prev is None or active < self.COMPACT_MIN_KEEP * prev:
+                return False   # most lanes active, or a collapsing population that finishes on its own
+            occupied = int((self.status.view(-1, 64) == _lib.ACTIVE).any(1).sum().item())
+            if occupied < 2 * (-(-int(active) // 64) + 2):
+                return False   # already dense
+        self.compact()
+        return True
+
+    def compact(self):
+        """Permute the lanes so that each lane range the kernels launch over (the serial schedule's batch, the
+        pipelined schedule's halves H0 / H1) holds its active lanes first, in their order, and the finished ones
+        behind them; waves of finished lanes then exit at once.  Every per-lane buffer moves with its lane (the
+        state and trajectory buffers, gains, per-lane scalars, histories, per-lane references) and ``lane_order``
+        follows, so solve() returns every lane in the caller's order: the results are the uncompacted solve's
+        bit for bit (each lane's arithmetic is its own).  Only lanes that change position are moved.  Lanes keep
+        their half: H0's sweep of the next iteration has already run when the pipelined loop synchronises."""
+        B, Bp, dev = self.B, self.Bp, self.eng.device
+        act = self.status[:B] == _lib.ACTIVE
+        perm = torch.arange(Bp, device=dev)
+        if self.pipeline:
+            Bh = C.c_int64()
+            _lib.check(self.eng.lib.gym_newton_pipeline_split(C.byref(self.batch), C.byref(Bh)),
+                       "gym_newton_pipeline_split")
+            ranges = [(0, int(Bh.value)), (int(Bh.value), B)]
+        else:
+            ranges = [(0, B)]
+        for lo, hi in ranges:
+            if hi > lo:   # active lanes first, each group in its present order
+                perm[lo:hi] = torch.argsort((~act[lo:hi]).to(torch.int8), stable=True) + lo
+        moved = (perm != torch.arange(Bp, device=dev)).nonzero().flatten()
+        if moved.numel() == 0:
+            return
+        src = perm[moved]
+        gd, jd, gs, js = moved // 64, moved % 64, src // 64, src % 64
+        for t in (self.x[0], self.x[1], self.K1):   # wave-blocked pairs (rows, Bp/64, 2, 64, 2)
+            v = t.view(t.shape[0], Bp // 64, 2, 64, 2)
+            v[:, gd, :, jd, :] = v[:, gs, :, js, :]
+        for t in (self.u[0], self.u[1], self.cs):   # planes (rows, 2, Bp)
+            v = t.view(t.shape[0], 2, Bp)
+            v[:, :, moved] = v[:, :, src]
+        for t in (self.cost, self.dJ, self.smax, self.gamma, self.status, self.n_iter, self.res_buf, self.n_roll):
+            t[moved] = t[src]
+        for t in (self.hist_cost, self.hist_smax):
+            if t is not None:
+                t[:, moved] = t[:, src]
+        if self.ref_lane:
+            self.xr_buf[moved] = self.xr_buf[src]
+            self.ur_buf[moved] = self.ur_buf[src]
+        order = self.lane_order if self.lane_order is not None else torch.arange(B, device=dev)
+        self.lane_order = order[perm[:B]]
+        self.compactions += 1
+
     # --- full solve ----------------------------------------------------------------------
     def solve(self, x0, max_iters: int, reduce_stats=None, sync_every: int = 1, log_every: int = 0,
               keep_stats: bool = False) -> SolveResult:
@@ -478,12 +557,19 @@ class BatchedNewtonSolver:
             inv[perm] = torch.arange(self.B, device=perm.device)
             self._capture_start(inv[torch.as_tensor(self.capture_lanes, device=perm.device)].tolist())
         self.tail_lane_its = 0
+        self.compactions = 0
+        self._compact_prev = None
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:
-            log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every,
-                              log_every=log_every, keep_stats=keep_stats)
+            self.lane_order_live = True
+            try:
+                log = newton_loop(self, max_iters, reduce_stats=reduce_stats, sync_every=sync_every,
+                                  log_every=log_every, keep_stats=keep_stats)
+            finally:
+                self.lane_order_live = False
         B = self.B
+        perm = self.lane_order   # the Morton order, composed with any lane compaction of the loop
         if perm is None:
             back = slice(0, B)
         else:   # internal lane i is input lane perm[i]: finalize writes row perm[i]; gather the scalars back
@@ -509,6 +595,7 @@ class BatchedNewtonSolver:
         res["sigmas"] = self.captured_sigmas() if self.capture_lanes is not None else None
         res["schedule"] = self.schedule
         res["tail_lane_iterations"] = int(self.tail_lane_its)
+        res["compactions"] = int(self.compactions)
         return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
                            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)
 
@@ -575,9 +662,11 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
     lane of any rank is active.  Returns the list of host statistics if ``keep_stats``."""
     log = []
     tail = int(getattr(stepper, "tail_lanes", 0) or 0)
+    compact = getattr(stepper, "maybe_compact", None) if getattr(stepper, "lane_order_live", False) else None
     for k in range(int(max_iters)):
         st = stepper.iteration()
         if (k + 1) % sync_every == 0 or k + 1 == max_iters:
+            local = st
             if reduce_stats is not None:
                 st = reduce_stats(st)
             host = st.cpu().numpy() if isinstance(st, torch.Tensor) else np.asarray(st)
@@ -598,6 +687,8 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
             if tail and host[0] <= tail and k + 1 < max_iters:
                 log += tail_loop(stepper, k + 1, int(max_iters), reduce_stats, log_every, keep_stats)
                 break
+            if compact is not None and k + 1 < max_iters:   # rank-local: no collective depends on it
+                compact(int(local[0].item()) if reduce_stats is not None else int(host[0]))
     return log
 
 

@@ -122,3 +122,30 @@ def test_straggler_tail_on_short_and_ragged_horizons(N):
     assert s.launches["tail"] > 0
     for f in FIELDS:
         _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"N={N}: {f}")
+
+
+@pytest.mark.parametrize("kind", ["pipelined", "serial", "per_lane_noreorder"])
+def test_lane_compaction_is_invisible(kind):
+    """Lane compaction (BatchedNewtonSolver.compact: each launch range's active lanes moved to its front, every
+    per-lane buffer and the lane order with them) at every host synchronisation ("force"), against the same solve
+    without it: every output bit for bit, in the caller's lane order -- on the pipelined schedule (lanes keep their
+    half), the serial one, and with per-lane references and no Morton reordering; then the straggler tail."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    B, max_iters = 1000, 200
+    x0 = _hard_lanes(B, seed=3)
+    xr, ur = _refs("task2")
+    skw = dict(pipeline=kind == "pipelined", reorder=kind != "per_lane_noreorder", tail_lanes=40)
+    if kind == "per_lane_noreorder":
+        xr = np.broadcast_to(xr, (B,) + xr.shape).copy()
+        ur = np.broadcast_to(ur, (B,) + ur.shape).copy()
+        ur[1::3, :, 1] *= 0.8
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, hist_len=max_iters, **skw)
+    r = BatchedNewtonSolver(eng, xr, ur, B, compact=False, **kw).solve(x0, max_iters, sync_every=3)
+    s = BatchedNewtonSolver(eng, xr, ur, B, compact="force", **kw)
+    t = s.solve(x0, max_iters, sync_every=3)
+    assert t.compactions > 5 and r.compactions == 0
+    for f in FIELDS:
+        _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{kind}: {f}")
+    assert t.iterations == r.iterations
