@@ -498,7 +498,9 @@ def main():
                 "every Armijo trial at once (bitwise the serial schedule, tests/test_gpu_tail.py)"}
     out["lane_compaction"] = {
         "enabled": bool(sv.compact_mode), "compactions_per_step": main_leg.compactions / max(a.steps, 1),
-        "note": "active lanes moved to the front of each launch range when few remain spread over many wavefronts "
+        "serial_from_iteration": sv.serial_switch_at,
+        "note": "once at most a quarter of the lanes stay active: a pipelined solve continues on the serial schedule "
+                "(its sweep storing sigma1) and the active lanes move to the front when spread over many wavefronts "
                 "(BatchedNewtonSolver.maybe_compact; bitwise invisible, tests/test_gpu_tail.py)"}
 
     kern, roof = main_leg.kernel_report(N)

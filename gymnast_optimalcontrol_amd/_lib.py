@@ -32,12 +32,13 @@ EXPORTS = (
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run",
                 "tail")
 
-ABI_VERSION = 10        # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 11        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
 FLAG_RUN_SINGLE = 4      # GYM_FLAG_RUN_SINGLE
 FLAG_REF_LANE = 8        # GYM_FLAG_REF_LANE
+FLAG_SIGMA_STREAM = 16   # GYM_FLAG_SIGMA_STREAM
 TRACK_SINGLE = 1         # GYM_TRACK_SINGLE
 CKPT_INTERVAL = 4        # GYM_CKPT_INTERVAL
 

@@ -3271,13 +3271,13 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
 #endif
 static void launch_post_trial(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                               const SolverCtl& c, const TrialIO& io, Range rg, int32_t* counter, double* stats_out,
-                              const double* other, double* total, hipStream_t st) {
+                              const double* other, double* total, hipStream_t st, bool sigma_streamed = false) {
     const int64_t n = rg.hi - rg.lo;
     const double2* K1 = (const double2*)b->K1;
     const double* cs = b->cs;
     double* hc = a->record_history ? b->hist_cost : nullptr;
     if (a->max_ls > 1 && n > 0) {
-        {   // the lanes that reject trial 1 need sigma1: re-run their sweep of this iteration into its plane
+        if (!sigma_streamed) {   // the lanes that reject trial 1 need sigma1: re-run their sweep into its plane
             TimedLaunch tl(b->timing, 7, st);
             hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, GYM_POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
                                kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
@@ -3317,9 +3317,13 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     const TrialIO io = trial_io(b, k);
     const int grid = grid_for(b->B, BLK);
     const bool hist = a->record_history != 0;
+    // GYM_FLAG_SIGMA_STREAM: the sweep also stores sigma1 (8 B per stage), so the lanes that reject trial 1 need no
+    // re-run of it (a chain as long as the sweep's, for however few lanes)
+    const bool sig = (b->flags & GYM_FLAG_SIGMA_STREAM) != 0;
     {
         TimedLaunch tl(b->timing, 0, st);
-        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_backward), dim3(grid), dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
+        hipLaunchKernelGGL(sig ? SERIAL_SEL(b, k_nt_backward_all) : SERIAL_SEL(b, k_nt_backward), dim3(grid),
+                           dim3(BLK), 0, st, Dyn(*m), kw(*w), io.x, io.u, b->x_ref, b->u_ref,
                            (double2*)b->K1, b->cs, a->gamma0, b->dJ, b->smax, b->status,
                            hist ? b->hist_smax : nullptr, all, b->Bp, b->N, k, b->hist_len);
     }
@@ -3331,7 +3335,7 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
                            b->n_iter, b->res_buf, b->n_roll, b->retry_list, b->counters, hist ? b->hist_cost : nullptr,
                            all, b->Bp, b->N);
     }
-    launch_post_trial(m, w, a, b, c, io, all, b->counters, b->stats, nullptr, nullptr, st);
+    launch_post_trial(m, w, a, b, c, io, all, b->counters, b->stats, nullptr, nullptr, st, sig);
     return launch_status();
 }
 

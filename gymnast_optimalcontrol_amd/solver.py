@@ -231,6 +231,8 @@ class BatchedNewtonSolver:
         self.compactions = 0
         self._compact_prev = None
         self.lane_order_live = False   # True inside solve(), whose results follow lane_order back
+        self._serial_now = False
+        self.serial_switch_at = None   # the iteration a pipelined solve continued on the serial schedule from
         self._tail_scratch = None
         self.tail_lane_its = 0
         self._cap_pos = None
@@ -292,6 +294,8 @@ class BatchedNewtonSolver:
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
         self._capture_start(self.capture_lanes or [])
+        self._serial_now = False   # a pipelined solve continues on the serial schedule after a lane compaction
+        self.batch.flags &= ~_lib.FLAG_SIGMA_STREAM
         if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
 
@@ -334,7 +338,7 @@ class BatchedNewtonSolver:
         k = self.k
         if self.persistent:
             self._run(k, k + 1)
-        elif self.pipeline:
+        elif self.pipeline and not self._serial_now:
             more = self.max_iters is None or k + 1 < self.max_iters
             self._phase(2 * k + 1, True)         # sweep H1 (iteration k) beside trial H0 (iteration k)
             self._phase(2 * k + 2, more)         # sweep H0 (iteration k+1) beside trial H1 (iteration k)
@@ -471,11 +475,14 @@ class BatchedNewtonSolver:
     COMPACT_MIN_KEEP = 0.5     # ... and the active count kept at least half its value since the last sync
 
     def maybe_compact(self, active: int) -> bool:
-        """At a host synchronisation (iteration boundary): compact the lanes if few remain active but they are
-        spread over many wavefronts.  A wavefront runs its whole chains while any of its 64 lanes is active, so
-        late in a hard solve (SURVEY 8(d)'s stress batch: ~22,000 of 262,144 lanes active for hundreds of
-        iterations) every SIMD still runs its four wavefronts for a few lanes each.  ``active``: this rank's count.
-        The trigger is rank-local (compaction changes no collective)."""
+        """At a host synchronisation (iteration boundary), once at most a quarter of the lanes stay active (a stable
+        population: the count kept at least half its value since the last sync): compact the lanes if they are
+        spread over many wavefronts, and continue a pipelined solve on the serial schedule.  A wavefront runs its
+        whole chains while any of its 64 lanes is active, so late in a hard solve (SURVEY 8(d)'s stress batch:
+        ~22,000 of 262,144 lanes active for hundreds of iterations) every SIMD may still run its four wavefronts for
+        a few lanes each; and with at most one wavefront per SIMD every launch is a latency-bound chain, where the
+        serial schedule runs the post-trial chains once per iteration instead of once per pipeline half.
+        ``active``: this rank's count.  The trigger is rank-local (neither step changes a collective)."""
         if not self.compact_mode:
             return False
         prev, self._compact_prev = self._compact_prev, int(active)
@@ -485,23 +492,40 @@ class BatchedNewtonSolver:
             if active > self.COMPACT_MAX_SHARE * self.B or prev is None or active < self.COMPACT_MIN_KEEP * prev:
                 return False   # most lanes active, or a collapsing population that finishes on its own
             occupied = int((self.status.view(-1, 64) == _lib.ACTIVE).any(1).sum().item())
-            if occupied < 2 * (-(-int(active) // 64) + 2):
-                return False   # already dense
+            if occupied < 2 * (-(-int(active) // 64) + 2):   # already dense: at most switch to serial
+                if not (self.pipeline and not self._serial_now):
+                    return False
+                self._to_serial()
+                return True
         self.compact()
         return True
 
-    def compact(self):
+    def _to_serial(self):
+        """Continue a pipelined solve on the serial schedule (see compact), its sweep storing sigma1."""
+        if self.pipeline and not self._serial_now:
+            self.serial_switch_at = self.k
+        self._serial_now = True
+        self.batch.flags |= _lib.FLAG_SIGMA_STREAM
+
+    def compact(self, to_serial: bool = True):
         """Permute the lanes so that each lane range the kernels launch over (the serial schedule's batch, the
         pipelined schedule's halves H0 / H1) holds its active lanes first, in their order, and the finished ones
         behind them; waves of finished lanes then exit at once.  Every per-lane buffer moves with its lane (the
         state and trajectory buffers, gains, per-lane scalars, histories, per-lane references) and ``lane_order``
         follows, so solve() returns every lane in the caller's order: the results are the uncompacted solve's
-        bit for bit (each lane's arithmetic is its own).  Only lanes that change position are moved.  Lanes keep
-        their half: H0's sweep of the next iteration has already run when the pipelined loop synchronises."""
+        bit for bit (each lane's arithmetic is its own).  Only lanes that change position are moved.
+        ``to_serial`` (the default): a pipelined solve continues on the serial schedule (the next iteration re-runs
+        H0's sweep, which the pipeline had already run: the same values), and the whole batch is one range.  With
+        at most a quarter of the lanes active every wavefront has a SIMD to itself, both schedules are chains of
+        latency-bound launches, and the serial one runs the post-trial chains (sigma1 re-run, candidates, accepted
+        re-run) once per iteration instead of once per half.  Otherwise lanes keep their pipeline half."""
         B, Bp, dev = self.B, self.Bp, self.eng.device
         act = self.status[:B] == _lib.ACTIVE
         perm = torch.arange(Bp, device=dev)
-        if self.pipeline:
+        pipelined = self.pipeline and not self._serial_now and not to_serial
+        if to_serial:   # the serial iteration's sweep then also stores sigma1 (no re-run for rejecting lanes)
+            self._to_serial()
+        if pipelined:
             Bh = C.c_int64()
             _lib.check(self.eng.lib.gym_newton_pipeline_split(C.byref(self.batch), C.byref(Bh)),
                        "gym_newton_pipeline_split")
@@ -559,6 +583,7 @@ class BatchedNewtonSolver:
         self.tail_lane_its = 0
         self.compactions = 0
         self._compact_prev = None
+        self.serial_switch_at = None
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 10
+#define GYM_ABI_VERSION 11
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -66,6 +66,10 @@ extern "C" {
                               * (gym_newton_init / _iteration / _phase / _run / _sigma / _finalize) and
                               * gym_newton_gamma_sweep; X_CKPT with it: GYM_EINVAL.  Same per-lane
                               * arithmetic as a shared reference (vector instead of scalar loads: the same bits). */
+#define GYM_FLAG_SIGMA_STREAM 16 /* gym_newton_iteration: the backward sweep also stores sigma1 (the cs plane 1),
+                                  * so the lanes that reject Armijo trial 1 skip the sigma1 re-run; the same values.
+                                  * For a few latency-bound lanes that backtrack often (the solver sets it after a
+                                  * lane compaction); ignored by the other schedules. */
 #define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 
