@@ -2475,9 +2475,14 @@ constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / ex
 constexpr bool TL_SPLIT = GYM_TAIL_SPLIT && !GYM_TAIL_QUAD;
 constexpr int TL_THREADS = TL_SPLIT ? 2 * BLK : BLK;
 constexpr int TL_GK = 6;         // doubles per stage in the gain ring: k row 1 (4), G11, 1/G11
+// TL_SPLIT trials: wavefront 0 runs the candidates' RK4 chains on lane pairs and hands each stage's (x_{t+1}, u1_t)
+// to wavefront 1 through a ring of 2 chunks x TL_RC stages x 32 trials x 3 pairs; wavefront 1 (lane c: trial c)
+// accumulates the cost and stores the candidate
+constexpr int TL_RC = 2;
+constexpr int TL_RING = 2 * TL_RC * (BLK / 2) * 3 * 2;   // doubles
 constexpr size_t tail_lds_bytes(int T) {
     return TL_SPLIT ? sizeof(double) * ((size_t)3 * TL_STAGES * TL_PITCH + (size_t)2 * TL_STAGES * TL_GK + 4 +
-                                        (size_t)T * TL_TST)
+                                        (size_t)TL_RING + (size_t)T * TL_TST)
                     : sizeof(double) * ((size_t)TL_STAGES * TL_PITCH + (size_t)(BLK / 4) * QX_DOUBLES +
                                         (size_t)T * TL_TST);
 }
@@ -2711,6 +2716,103 @@ __device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, i
     return J + xcost(ka.w.QT, n0, n1, n2, n3, xrT.v);
 }
 
+// TL_SPLIT, wavefront 0: the RK4 chain of Armijo trial c on the lane pair (2c, 2c + 1) -- the offset-form feedback
+// and gym::rk4_pair, exactly tail_candidate's chain -- handing each stage's state and control to wavefront 1 (ring
+// [chunk & 1][stage in chunk][trial][(th1, th2) | (w1, w2) | (u1, -)]).  Chunk cc between barriers cc and cc + 1.
+typedef double2 (*tring_t)[TL_RC][BLK / 2][3];
+template <bool U0Z, bool RL>
+__device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring, int64_t l, int cb, int c, double g,
+                                                 bool odd) {
+    const targs_t R = tail_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double dg = g - R->a.gamma0;
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    const KArgs ka = kernarg_consts();
+    const Dyn m = ka.m;
+    const int nch = (T + TL_RC - 1) / TL_RC;
+    const int tc = c < BLK / 2 ? c : 0;
+    for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+        for (int j = 0; j < TL_RC; ++j) {
+            const int t = cc * TL_RC + j;
+            if (t < T) {
+                const double* q = tst + t * TL_TST;
+                const double2 k0 = make_double2(q[0], q[1]), k1 = make_double2(q[2], q[3]);
+                const double y = trial_u1(k0, k1, q[4], n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
+                const double ysig = __builtin_fma(dg, q[5], y);             // trial_u1_sig's value
+                const double u1 = c == 0 ? y : ysig;
+                gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
+                double2* r = ring[cc & 1][j][tc];
+                if (odd) r[1] = make_double2(n2, n3);
+                else { r[0] = make_double2(n0, n1); r[2] = make_double2(u1, 0.0); }
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();                       // the helper's last chunk
+}
+
+// TL_SPLIT, wavefront 1, lane c (< max_ls): trial c's cost (stage costs in stage order, as tail_candidate) and its
+// candidate trajectory into virtual lane v of the scratch; returns J.  Chunk cc between barriers cc + 1 and cc + 2.
+template <bool U0Z, bool RL>
+__device__ __forceinline__ double tail_trial_helper(const double* tst, tring_t ring, int64_t l, int cb, int c, double g,
+                                                    int64_t v, bool act) {
+    const targs_t R = tail_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
+    const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
+    const uint32_t v2 = wbo(v, 2), v1o = (uint32_t)v * 8u;
+    const uint32_t srow = (uint32_t)R->Vp * 16u, splane = (uint32_t)R->Vp * 8u;
+    const char* Xs = reinterpret_cast<const char*>(R->sx);
+    const char* Us = reinterpret_cast<const char*>(R->su);
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    if (act) {
+        const auto rX = rsrc(Xs);
+        bst2(rX, v2, 0, n0, n1);
+        bst2(rX, v2, WROW, n2, n3);
+    }
+    double J = 0.0;
+    const KArgs ka = kernarg_consts();
+    const double G00 = ka.w.G00, iG00 = ka.w.iG00;
+    const int nch = (T + TL_RC - 1) / TL_RC;
+    const int tc = c < BLK / 2 ? c : 0;
+    __syncthreads();                       // the chain's chunk 0
+    for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+        for (int j = 0; j < TL_RC; ++j) {
+            const int t = cc * TL_RC + j;
+            if (t < T) {
+                const double2* r = ring[cc & 1][j][tc];
+                const double2 na = r[0], nb = r[1], uu = r[2];
+                const Row<2> urt = ref_row<2, RL>(ur, t);
+                const Row<4> xrt = ref_row<4, RL>(xr, t);
+                const double v0 = U0Z ? 0.0 : trial_u0(tst[t * TL_TST + 6], urt.v[0], g, G00, iG00);
+                const double u1 = uu.x;
+                const double f0 = U0Z ? 0.0 : v0 - urt.v[0], f1 = u1 - urt.v[1];
+                const KArgs kc = kernarg_consts();
+                J = stage_cost<U0Z>(J, kc.w.Q, kc.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
+                if (act) {
+                    const auto rO = rsrc(Us + (int64_t)t * srow);
+                    if (!U0Z) bst1(rO, v1o, 0, v0);
+                    bst1(rO, v1o, splane, u1);
+                    const auto rX = rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow));
+                    bst2(rX, v2, 0, na.x, na.y);
+                    bst2(rX, v2, WROW, nb.x, nb.y);
+                }
+                n0 = na.x; n1 = na.y; n2 = nb.x; n3 = nb.y;
+            }
+        }
+        __syncthreads();
+    }
+    const Row<4> xrT = ref_row<4, RL>(xr, T);
+    return J + xcost(ka.w.QT, n0, n1, n2, n3, xrT.v);
+}
+
 #ifdef GYM_TAIL_TRACE
 // Diagnostic build only (tools/tail_trace.py): per workgroup, cycles (s_memtime) in the sweep, the trials, the rest
 // of the iteration, and the iterations run
@@ -2724,7 +2826,8 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
     double* xq = lin + TL_STAGES * TL_PITCH;
     double* gk2 = lin + 3 * TL_STAGES * TL_PITCH;
     double* shd = gk2 + 2 * TL_STAGES * TL_GK;
-    double* tst = TL_SPLIT ? shd + 4 : xq + (BLK / 4) * QX_DOUBLES;
+    const tring_t ring = reinterpret_cast<tring_t>(shd + 4);   // TL_SPLIT with PAIR: the trials' hand-off
+    double* tst = TL_SPLIT ? shd + 4 + TL_RING : xq + (BLK / 4) * QX_DOUBLES;
     const int lane = threadIdx.x & (BLK - 1);
     const int wave = threadIdx.x / BLK;           // TL_SPLIT: 0 the matrix half and the trials, 1 the vector half
     const int64_t l = tail_args()->list[blockIdx.x];
@@ -2754,13 +2857,25 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
         }
         __syncthreads();   // the staged trial inputs (LDS) complete
         const int max_ls = tail_args()->a.max_ls;
-        const int cand = PAIR ? lane >> 1 : lane;   // this thread's trial (PAIR: on lanes 2c, 2c + 1)
+        // TL_SPLIT with lane pairs: wavefront 0 runs the trials' chains (trial c on lanes 2c, 2c + 1), wavefront 1
+        // (lane c: trial c) their costs, stores and Armijo tests; otherwise wavefront 0 does all of it
+        constexpr bool HELPER = TL_SPLIT && PAIR;
+        const int dec = HELPER ? 1 : 0;             // the wavefront holding the decisions
+        const int cand = (PAIR && !(HELPER && wave == 1)) ? lane >> 1 : lane;   // this thread's trial
         const int64_t v = (int64_t)blockIdx.x * max_ls + cand;
         double g = tail_args()->a.gamma0;
         for (int q = 0; q < cand && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
         bool ok = false;
         double Jn = 0.0;
-        if (cand < max_ls && wave == 0) {
+        if (HELPER) {
+            if (wave == 0) {
+                tail_trial_chain<U0Z, RL>(tst, ring, l, cb, cand, g, lane & 1);
+            } else {
+                Jn = tail_trial_helper<U0Z, RL>(tst, ring, l, cb, cand, g, v, cand < max_ls);
+                const targs_t R = tail_args();
+                ok = cand < max_ls && Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
+            }
+        } else if (cand < max_ls && wave == 0) {
             Jn = tail_candidate<U0Z, RL, PAIR>(tst, l, cb, cand, g, v, lane & 1);
             const targs_t R = tail_args();
             ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
@@ -2768,16 +2883,16 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
         const unsigned long long okm = __ballot(ok);
         acc[1] += R2T_NOW() - tt;
         tt = R2T_NOW();
-        // the first accepted trial, in order (PAIR: both lanes of a pair hold the same decision); TL_SPLIT: wavefront
-        // 0's, handed to wavefront 1 so that both leave the iteration loop together
-        int first = okm ? (__ffsll((long long)okm) - 1) / (PAIR ? 2 : 1) : -1;
+        // the first accepted trial, in order (PAIR without the helper: both lanes of a pair hold the same decision);
+        // TL_SPLIT: handed from the deciding wavefront to the other so that both leave the iteration loop together
+        int first = okm ? (__ffsll((long long)okm) - 1) / ((PAIR && !HELPER) ? 2 : 1) : -1;
+        lane_fence();   // the candidates' scratch stores, before the copy reads them
         if (TL_SPLIT) {
-            if (wave == 0 && lane == 0) shd[2] = (double)first;
+            if (wave == dec && lane == 0) shd[2] = (double)first;
             __syncthreads();
             first = (int)shd[2];
         }
         const int nr = first >= 0 ? first + 1 : max_ls;
-        lane_fence();   // the candidates' scratch stores, before the copy reads them
         if (first >= 0 && wave == 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
             const targs_t R = tail_args();
             const int T = R->N - 1;
@@ -2811,10 +2926,10 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
                 }
             }
         }
-        const int src = (first >= 0 ? first : 0) * (PAIR ? 2 : 1);
+        const int src = (first >= 0 ? first : 0) * ((PAIR && !HELPER) ? 2 : 1);
         const double Jf = __shfl(Jn, src);
         const double gf = __shfl(g, src);
-        if (lane == 0 && wave == 0) {
+        if (lane == 0 && wave == dec) {
             const targs_t F = tail_args();
             F->n_roll[l] += nr;
             F->n_iter[l] += 1;
