@@ -545,6 +545,7 @@ def main():
             "roofline": None if rg is None else {k: rg[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
                                                                      "bytes_per_unit")},
             "specialisation_share": 1.0 - leg.value / value,
+            "serial_from_iteration": leg.solver.serial_switch_at, "compactions_per_step": leg.compactions / a.extra_steps,
             "note": "the same workload on the general kernels (u0_zero off: the tau1 planes are read and written, "
                     "as for any reference with a live tau1 channel such as task 1); bitwise-identical results "
                     "(tests/test_gpu_parity.py::test_u0_zero_stream_skipping_is_bitwise_identical)"}
