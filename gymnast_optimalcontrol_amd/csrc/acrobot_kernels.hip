@@ -1690,8 +1690,9 @@ struct RunArgs {
     double *cost, *dJ, *smax, *gamma;
     int32_t *status, *n_iter, *res_buf, *n_roll;
     double *hist_cost, *hist_smax;
+    int32_t *retry_list, *counter;   // ext: the lanes that reject trial 1 (GYM_FLAG_SIGMA_STREAM)
     int64_t B, Bp;
-    int32_t N, k0, k1, pad;
+    int32_t N, k0, k1, ext;
 };
 static_assert(offsetof(RunArgs, w) == 96, "kernarg layout: KW at byte 96 (kernarg_consts)");
 typedef const RunArgs* rargs_t;   // generic pointer into the kernarg segment (inferred back to scalar loads)
@@ -2072,6 +2073,7 @@ template <bool U0Z, bool RL>
 __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int lane, int64_t l, int cb, bool act,
                                                double& dJ_out, double& smax_out, unsigned long long& bw) {
     const rargs_t R = run_args();
+    const bool ext = R->ext != 0;
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
     const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
@@ -2100,8 +2102,14 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
                             qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
                 double s0, s1;
                 S.step_p<U0Z>(ka.w, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
-                if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
-                                                 ka01.y, ka23.x, ka23.y, s1);
+                if (act) {
+                    if (ext)   // external retries: sigma1 stored too (the candidates read it; no re-run)
+                        store_stage<OUT_ALL>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
+                                             ka01.y, ka23.x, ka23.y, s1);
+                    else
+                        store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
+                                                ka01.y, ka23.x, ka23.y, s1);
+                }
             }
         }
         lds_barrier(bw);
@@ -2359,7 +2367,13 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
             double g = R->a.gamma0;
             int nr = 1;
             bool ok = Jn < R->cost[l] + R->a.c * g * R->dJ[l];   // strict Armijo test (:361)
-            if (!ok && R->a.max_ls > 1) {
+            const bool deferred = !ok && R->a.max_ls > 1 && R->ext;
+            if (deferred) {
+                // external retries (one iteration per launch): the lane joins the retry list, as after the serial
+                // schedule's trial (k_nt_trial); the candidates / accepted re-run kernels finish its iteration
+                R->n_roll[l] += 1;
+                R->retry_list[atomicAdd(R->counter, 1)] = (int32_t)l;
+            } else if (!ok && R->a.max_ls > 1) {
                 lane_fence();                              // the helper's candidate stores, before they are rewritten
                 {
                     const rargs_t P = run_args();
@@ -2383,18 +2397,20 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
                     ok = Jn < Q->cost[l] + Q->a.c * g * Q->dJ[l];
                 }
             }
-            const rargs_t F = run_args();
-            F->n_roll[l] += nr;
-            F->n_iter[l] += 1;
-            SolverCtl c = F->a;
-            c.k = k;
-            if (ok) {
-                const double sm = F->smax[l];
-                accept_lane(c, l, Jn, g, sm, F->cost, F->gamma, F->status, F->res_buf, F->hist_cost, F->Bp);
-                if (sm < c.tol) st = GYM_CONVERGED;
-            } else {
-                fail_lane(c, l, F->status, F->res_buf);
-                st = GYM_LS_FAILED;
+            if (!deferred) {
+                const rargs_t F = run_args();
+                F->n_roll[l] += nr;
+                F->n_iter[l] += 1;
+                SolverCtl c = F->a;
+                c.k = k;
+                if (ok) {
+                    const double sm = F->smax[l];
+                    accept_lane(c, l, Jn, g, sm, F->cost, F->gamma, F->status, F->res_buf, F->hist_cost, F->Bp);
+                    if (sm < c.tol) st = GYM_CONVERGED;
+                } else {
+                    fail_lane(c, l, F->status, F->res_buf);
+                    st = GYM_LS_FAILED;
+                }
             }
         }
         if (!helper) shst[lane] = st;
@@ -3503,11 +3519,34 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
 
 int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b, int32_t k0,
                    int32_t k1, void* s) {
-    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT))
+    // GYM_FLAG_SIGMA_STREAM with the four-wavefront kernel: one iteration per launch, its sweep storing sigma1, the
+    // lanes that reject trial 1 finished by the serial schedule's parallel candidates and accepted re-run
+    const bool ext = (b->flags & GYM_FLAG_SIGMA_STREAM) && !(b->flags & GYM_FLAG_RUN_SINGLE) && R2SPLIT;
+    if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT) || (ext && k1 > k0 + 1))
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;
     const bool hist = a->record_history != 0;
     const SolverCtl c{a->tol, a->beta, a->c, a->gamma0, a->max_ls, k0, b->hist_len, 0};
+    if (ext) {
+        if (k1 > k0) {
+            TimedLaunch tl(b->timing, 8, st);
+            RunArgs ra;
+            ra.m = Dyn(*m);
+            ra.w = kw(*w);
+            ra.a = c;
+            for (int i = 0; i < 2; ++i) { ra.x[i] = (double2*)b->x[i]; ra.u[i] = b->u[i]; }
+            ra.K1 = (double2*)b->K1; ra.cs = b->cs; ra.xr = b->x_ref; ra.ur = b->u_ref;
+            ra.cost = b->cost; ra.dJ = b->dJ; ra.smax = b->smax; ra.gamma = b->gamma;
+            ra.status = b->status; ra.n_iter = b->n_iter; ra.res_buf = b->res_buf; ra.n_roll = b->n_roll;
+            ra.hist_cost = hist ? b->hist_cost : nullptr; ra.hist_smax = hist ? b->hist_smax : nullptr;
+            ra.retry_list = b->retry_list; ra.counter = b->counters;
+            ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.ext = 1;
+            hipLaunchKernelGGL(RUN_SEL(b, k_nt_run2), dim3((unsigned)(b->Bp / BLK)), dim3(R2WAVES * BLK), 0, st, ra);
+            launch_post_trial(m, w, a, b, c, trial_io(b, k0), Range{0, b->B}, b->counters, b->stats, nullptr,
+                              nullptr, st, true);
+            return launch_status();
+        }
+    }
     if (k1 > k0) {
         TimedLaunch tl(b->timing, 8, st);
         RunArgs ra;
@@ -3519,7 +3558,8 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
         ra.cost = b->cost; ra.dJ = b->dJ; ra.smax = b->smax; ra.gamma = b->gamma;
         ra.status = b->status; ra.n_iter = b->n_iter; ra.res_buf = b->res_buf; ra.n_roll = b->n_roll;
         ra.hist_cost = hist ? b->hist_cost : nullptr; ra.hist_smax = hist ? b->hist_smax : nullptr;
-        ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.pad = 0;
+        ra.retry_list = b->retry_list; ra.counter = b->counters;
+        ra.B = b->B; ra.Bp = b->Bp; ra.N = b->N; ra.k0 = k0; ra.k1 = k1; ra.ext = ext ? 1 : 0;
         if (b->flags & GYM_FLAG_RUN_SINGLE)
             hipLaunchKernelGGL(RUN_SEL(b, k_nt_run), dim3(grid_for(b->B, BLK)), dim3(BLK), 0, st, ra);
         else   // two wavefronts per 64 lanes; every lane of the padded batch takes part (padding: GYM_PAD)

@@ -232,7 +232,8 @@ class BatchedNewtonSolver:
         self._compact_prev = None
         self.lane_order_live = False   # True inside solve(), whose results follow lane_order back
         self._serial_now = False
-        self.serial_switch_at = None   # the iteration a pipelined solve continued on the serial schedule from
+        self._run_now = False
+        self.serial_switch_at = None   # the iteration the low-occupancy switch happened at
         self._tail_scratch = None
         self.tail_lane_its = 0
         self._cap_pos = None
@@ -294,7 +295,8 @@ class BatchedNewtonSolver:
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
         self._capture_start(self.capture_lanes or [])
-        self._serial_now = False   # a pipelined solve continues on the serial schedule after a lane compaction
+        self._serial_now = False   # the low-occupancy switch (maybe_compact / _to_serial)
+        self._run_now = False
         self.batch.flags &= ~_lib.FLAG_SIGMA_STREAM
         if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
@@ -336,7 +338,7 @@ class BatchedNewtonSolver:
     def iteration(self) -> torch.Tensor:
         """Enqueue outer iteration k for every active lane; returns the 8 total statistics (device)."""
         k = self.k
-        if self.persistent:
+        if self.persistent or self._run_now:
             self._run(k, k + 1)
         elif self.pipeline and not self._serial_now:
             more = self.max_iters is None or k + 1 < self.max_iters
@@ -492,19 +494,24 @@ class BatchedNewtonSolver:
             if active > self.COMPACT_MAX_SHARE * self.B or prev is None or active < self.COMPACT_MIN_KEEP * prev:
                 return False   # most lanes active, or a collapsing population that finishes on its own
             occupied = int((self.status.view(-1, 64) == _lib.ACTIVE).any(1).sum().item())
-            if occupied < 2 * (-(-int(active) // 64) + 2):   # already dense: at most switch to serial
-                if not (self.pipeline and not self._serial_now):
-                    return False
+            if occupied < 2 * (-(-int(active) // 64) + 2) and (self._serial_now or not self.split_waves):
+                if self._serial_now:
+                    return False           # already dense, already switched
                 self._to_serial()
                 return True
-        self.compact()
+        self.compact()                     # (entering the persistent kernel's mode: always dense first)
         return True
 
     def _to_serial(self):
-        """Continue a pipelined solve on the serial schedule (see compact), its sweep storing sigma1."""
-        if self.pipeline and not self._serial_now:
+        """Continue a pipelined or serial solve one iteration per launch of the four-wavefront persistent kernel
+        (k_nt_run2: split Riccati sweep, lane-pair trial chains), its sweep storing sigma1 and the lanes that reject
+        trial 1 finished by the serial schedule's parallel candidates and accepted re-run (GYM_FLAG_SIGMA_STREAM);
+        with single-wavefront persistent kernels (split_waves=False), on the serial schedule (its sweep storing
+        sigma1).  The same bits either way (the schedules' bitwise equality)."""
+        if not self._serial_now:
             self.serial_switch_at = self.k
         self._serial_now = True
+        self._run_now = self.split_waves
         self.batch.flags |= _lib.FLAG_SIGMA_STREAM
 
     def compact(self, to_serial: bool = True):

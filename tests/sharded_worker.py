@@ -37,8 +37,23 @@ def main():
     lo3, hi3, r3 = gd.solve_sharded(x0, xr3, ur3, 40, tol=1e-4, gamma_0=0.1)
     np.savez(f"{out}.perlane.rank{rank}.npz", lo=lo3, hi=hi3, x=r3.x.cpu().numpy(), cost=r3.cost.cpu().numpy(),
              n_iter=r3.n_iter.cpu().numpy())
+    if total > 1000:   # hard lanes with lane compaction forced at every sync (rank-local) and the tail (global)
+        xh = hard_x0(2000, 3)
+        _, _, gh = gd.solve_sharded(xh, x_ref, u_ref, 200, gather=True, tol=1e-4, gamma_0=0.1, compact="force",
+                                    tail_lanes=60, hist_len=200)
+        np.savez(f"{out}.hard.rank{rank}.npz", **{k: v.cpu().numpy() for k, v in gh.items()})
     dist.barrier()
     dist.destroy_process_group()
+
+
+def hard_x0(total: int, seed: int) -> np.ndarray:
+    """SURVEY 8(d)'s stress distribution (theta0 ~ U(+-1.5), some initial velocities) with a NaN lane."""
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((total, 4))
+    x0[:, :2] = rng.uniform(-1.5, 1.5, (total, 2))
+    x0[::9, 2:] = rng.uniform(-2.0, 2.0, (len(x0[::9]), 2))
+    x0[7] = np.nan
+    return x0
 
 
 def sharded_x0(total: int, seed: int) -> np.ndarray:

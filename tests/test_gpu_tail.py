@@ -124,18 +124,22 @@ def test_straggler_tail_on_short_and_ragged_horizons(N):
         _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"N={N}: {f}")
 
 
-@pytest.mark.parametrize("kind", ["pipelined", "serial", "per_lane_noreorder"])
+@pytest.mark.parametrize("kind", ["pipelined", "serial", "per_lane_noreorder", "serial_single_wave"])
 def test_lane_compaction_is_invisible(kind):
-    """Lane compaction (BatchedNewtonSolver.compact: each launch range's active lanes moved to its front, every
-    per-lane buffer and the lane order with them) at every host synchronisation ("force"), against the same solve
-    without it: every output bit for bit, in the caller's lane order -- on the pipelined schedule (lanes keep their
-    half), the serial one, and with per-lane references and no Morton reordering; then the straggler tail."""
+    """The low-occupancy switch forced at every host synchronisation (compact="force"): lane compaction
+    (BatchedNewtonSolver.compact: the active lanes moved to the front, every per-lane buffer and the lane order
+    with them) and the continuation one iteration per launch of the four-wavefront persistent kernel with external
+    retries (its sweep storing sigma1, the serial schedule's candidates and accepted re-run; GYM_FLAG_SIGMA_STREAM)
+    -- or, with split_waves=False, on the serial schedule with sigma1 streamed -- against the same solve without
+    it: every output bit for bit, in the caller's lane order; from the pipelined and the serial schedules, with
+    per-lane references and no Morton reordering; then the straggler tail."""
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
     from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
     B, max_iters = 1000, 200
     x0 = _hard_lanes(B, seed=3)
     xr, ur = _refs("task2")
-    skw = dict(pipeline=kind == "pipelined", reorder=kind != "per_lane_noreorder", tail_lanes=40)
+    skw = dict(pipeline=kind == "pipelined", reorder=kind != "per_lane_noreorder", tail_lanes=40,
+               split_waves=kind != "serial_single_wave")
     if kind == "per_lane_noreorder":
         xr = np.broadcast_to(xr, (B,) + xr.shape).copy()
         ur = np.broadcast_to(ur, (B,) + ur.shape).copy()
@@ -146,6 +150,7 @@ def test_lane_compaction_is_invisible(kind):
     s = BatchedNewtonSolver(eng, xr, ur, B, compact="force", **kw)
     t = s.solve(x0, max_iters, sync_every=3)
     assert t.compactions > 5 and r.compactions == 0
+    assert s.launches["run"] > 0 if kind != "serial_single_wave" else s.launches["run"] == 0
     for f in FIELDS:
         _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{kind}: {f}")
     assert t.iterations == r.iterations

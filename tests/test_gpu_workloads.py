@@ -217,7 +217,9 @@ def test_sharded_solve_on_hip_matches_unsharded(total, tmp_path):
     """Two ranks (gloo, sharing this GPU) run distributed.solve_sharded on the HIP solver.  65,537 lanes give
     ragged shards of 32,769 / 32,768 lanes on either side of the persistent-schedule threshold (128 lanes per CU
     on 256 CUs): both ranks must still pick the same schedule (chosen on the largest shard), pair up their
-    all-reduces, and reproduce the unsharded solve bit for bit; 301 lanes run the persistent schedule."""
+    all-reduces, and reproduce the unsharded solve bit for bit; 301 lanes run the persistent schedule.  With 65,537
+    lanes the worker also solves 2,000 hard lanes with lane compaction forced (rank-local) and the straggler tail
+    (switched on the global count): gathered, the unsharded solve's bits."""
     import torch
     from bench import load_refs
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
@@ -263,6 +265,16 @@ def test_sharded_solve_on_hip_matches_unsharded(total, tmp_path):
         lo, hi = int(p3["lo"]), int(p3["hi"])
         for k in ("x", "cost", "n_iter"):
             assert np.array_equal(p3[k], getattr(r3, k)[lo:hi].cpu().numpy(), equal_nan=True), (k, rk)
+    if total > 1000:   # hard lanes, lane compaction forced on each rank, the straggler tail: the unsharded solve's bits
+        from sharded_worker import hard_x0
+        xh = hard_x0(2000, 3)
+        rh = BatchedNewtonSolver(AcrobotEngine(), x_ref, u_ref, 2000, tol=1e-4, gamma_0=0.1, compact=False,
+                                 tail_lanes=0, hist_len=200).solve(xh, 200)
+        assert (rh.n_rollouts > rh.n_iter).sum() > 10
+        for rk in range(2):
+            gh = np.load(f"{out}.hard.rank{rk}.npz")
+            for k in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma"):
+                assert np.array_equal(gh[k], getattr(rh, k).cpu().numpy(), equal_nan=True), ("hard", k, rk)
     torch.cuda.synchronize()
 
 
