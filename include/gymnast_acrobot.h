@@ -68,8 +68,11 @@ extern "C" {
                               * arithmetic as a shared reference (vector instead of scalar loads: the same bits). */
 #define GYM_FLAG_SIGMA_STREAM 16 /* gym_newton_iteration: the backward sweep also stores sigma1 (the cs plane 1),
                                   * so the lanes that reject Armijo trial 1 skip the sigma1 re-run; the same values.
-                                  * For a few latency-bound lanes that backtrack often (the solver sets it after a
-                                  * lane compaction); ignored by the other schedules. */
+                                  * gym_newton_run (four-wavefront kernel): one iteration per launch (k1 = k0 + 1,
+                                  * else GYM_EINVAL), its sweep storing sigma1, the lanes that reject trial 1 put on
+                                  * the retry list and finished by the serial schedule's parallel candidates and
+                                  * accepted re-run in the same call.  The solver sets it in its low-occupancy
+                                  * regime; ignored by the pipelined phases. */
 #define GYM_CKPT_INTERVAL 4
 #define GYM_EINVAL 1  /* == hipErrorInvalidValue */
 
