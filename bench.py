@@ -218,7 +218,7 @@ class NewtonLeg:
         gd.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        lane_its, rolls, res, tail_its, compactions = 0, 0, None, 0, 0
+        lane_its, rolls, res, tail_its, compactions, lowocc_its = 0, 0, None, 0, 0, 0
         for _ in range(steps):
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
@@ -226,11 +226,13 @@ class NewtonLeg:
             rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
             tail_its += res.tail_lane_iterations
             compactions += res.compactions
+            lowocc_its += res.lowocc_lane_iterations
         torch.cuda.synchronize()
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
         self.res, self.lane_its, self.steps, self.tail_lane_its = res, lane_its, steps, tail_its
         self.compactions = compactions
+        self.lowocc_lane_its = lowocc_its
         self.elapsed = elapsed
         self.lane_its_all = int(gd.sum_over_ranks(lane_its))
         self.rollouts_all = int(gd.sum_over_ranks(rolls))
@@ -249,7 +251,7 @@ class NewtonLeg:
             if launches:
                 kern[kind] = {"avg_ms": ms / launches, "launches": launches}
         lane_its = self.lane_its
-        if "run" in kern:
+        if solver.persistent:
             # persistent schedule: every lane-iteration (sweep + trial) runs inside the run launches
             dom = "run"
             per_launch = lane_its * ab["iteration"] / kern["run"]["launches"]
@@ -258,13 +260,13 @@ class NewtonLeg:
             bytes_per_lane, unit_note = ab["iteration"], "sweep + trial of one lane-iteration"
         elif "phase_odd" in kern:
             # pipelined schedule: every lane-iteration = one sweep + one trial inside the phase launches (2 per
-            # outer iteration + 1 per solve; a launch's time is recorded whenever its timing slot is free) -- up to
-            # the straggler tail, whose lane-iterations are not in them
+            # outer iteration + 1 per solve) -- up to the low-occupancy switch and the straggler tail, whose
+            # lane-iterations are not in them
             dom = "phase"
             rec_ms = sum(kern[k]["avg_ms"] * kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
             rec_n = sum(kern[k]["launches"] for k in ("phase_odd", "phase_even") if k in kern)
             total_launches = solver.launches["phase"]
-            tail_its = self.tail_lane_its
+            tail_its = self.tail_lane_its + self.lowocc_lane_its
             per_launch = (lane_its - tail_its) * ab["iteration"] / total_launches
             kern["phase"] = {"avg_ms": rec_ms / rec_n, "launches": total_launches, "recorded": rec_n,
                              "algorithmic_bytes_per_launch": per_launch}
@@ -273,7 +275,8 @@ class NewtonLeg:
         else:
             for kind in ("backward", "trial"):
                 if kind in kern:
-                    per_launch = lane_its * ab[kind] / kern[kind]["launches"]
+                    per_launch = ((lane_its - self.tail_lane_its - self.lowocc_lane_its) * ab[kind] /
+                                  kern[kind]["launches"])
                     kern[kind]["algorithmic_bytes_per_launch"] = per_launch
                     kern[kind]["achieved_GBs"] = per_launch / (kern[kind]["avg_ms"] * 1e-3) / 1e9
             dom = max(("backward", "trial"), key=lambda k: kern.get(k, {}).get("avg_ms", 0))
@@ -499,9 +502,10 @@ def main():
     out["lane_compaction"] = {
         "enabled": bool(sv.compact_mode), "compactions_per_step": main_leg.compactions / max(a.steps, 1),
         "serial_from_iteration": sv.serial_switch_at,
-        "note": "once at most a quarter of the lanes stay active: a pipelined solve continues on the serial schedule "
-                "(its sweep storing sigma1) and the active lanes move to the front when spread over many wavefronts "
-                "(BatchedNewtonSolver.maybe_compact; bitwise invisible, tests/test_gpu_tail.py)"}
+        "lane_iterations_per_step": main_leg.lowocc_lane_its // max(a.steps, 1),
+        "note": "once at most a quarter of the lanes stay active: the active lanes move to the front and the solve "
+                "continues one iteration per launch of the persistent kernel with parallel Armijo retries "
+                "(BatchedNewtonSolver.maybe_compact, GYM_FLAG_SIGMA_STREAM; bitwise invisible, tests/test_gpu_tail.py)"}
 
     kern, roof = main_leg.kernel_report(N)
     if kern and rank == 0:

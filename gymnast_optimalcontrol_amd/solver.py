@@ -64,6 +64,7 @@ class SolveResult:
     schedule: str = ""                      # "serial" | "pipelined" | "persistent"
     tail_lane_iterations: int = 0           # lane-iterations run by the straggler tail (gym_newton_tail)
     compactions: int = 0                    # lane compactions during the loop (BatchedNewtonSolver.compact)
+    lowocc_lane_iterations: int = 0         # lane-iterations run in the low-occupancy regime (maybe_compact)
 
 
 class BatchedNewtonSolver:
@@ -234,6 +235,7 @@ class BatchedNewtonSolver:
         self._serial_now = False
         self._run_now = False
         self.serial_switch_at = None   # the iteration the low-occupancy switch happened at
+        self._its_switch, self._its_tail_start = 0, None
         self._tail_scratch = None
         self.tail_lane_its = 0
         self._cap_pos = None
@@ -510,6 +512,7 @@ class BatchedNewtonSolver:
         sigma1).  The same bits either way (the schedules' bitwise equality)."""
         if not self._serial_now:
             self.serial_switch_at = self.k
+            self._its_switch = int(self.n_iter[:self.B].sum().item())
         self._serial_now = True
         self._run_now = self.split_waves
         self.batch.flags |= _lib.FLAG_SIGMA_STREAM
@@ -591,6 +594,8 @@ class BatchedNewtonSolver:
         self.compactions = 0
         self._compact_prev = None
         self.serial_switch_at = None
+        self._its_switch = 0
+        self._its_tail_start = None
         if self.persistent:
             log = run_loop(self, int(max_iters), reduce_stats, log_every, keep_stats)
         else:
@@ -628,6 +633,11 @@ class BatchedNewtonSolver:
         res["schedule"] = self.schedule
         res["tail_lane_iterations"] = int(self.tail_lane_its)
         res["compactions"] = int(self.compactions)
+        lowocc = 0
+        if self.serial_switch_at is not None:   # up to the tail switch, or the end of the solve
+            end = self._its_tail_start if self._its_tail_start is not None else int(n_iter.sum().item())
+            lowocc = end - self._its_switch
+        res["lowocc_lane_iterations"] = int(lowocc)
         return SolveResult(x=x, u=u, K=K, sigma=s, n_iter=n_iter, iterations=iters,
                            lane_iterations=int(n_iter.sum().item()), seconds=secs, stats_log=log, **res)
 
@@ -730,6 +740,7 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
     all-reduced and read after each launch, and the loop stops when no lane of any rank is active."""
     log = []
     its0 = int(solver.n_iter[:solver.B].sum().item())
+    solver._its_tail_start = its0
     while k < max_iters:
         k1 = min(max_iters, k + solver.tail_chunk)
         st = solver.tail_run(k, k1)
