@@ -124,9 +124,16 @@ template <int CP = kNT>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a, double b) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, CP);
 }
+template <int CP = kNT>
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, kNT);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, CP);
 }
+// GYM_MALL_STAGES (measurement variant, default 0): the stages a pass writes last and the next pass reads first
+// (the sweep's lowest stages, the trial's highest knots) stored with the default cache policy instead of nt, so
+// that they may still be in the 256 MB Infinity Cache when the next phase starts
+#ifndef GYM_MALL_STAGES
+#define GYM_MALL_STAGES 0
+#endif
 
 __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 
@@ -344,16 +351,27 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
         J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
+        const bool keep = GYM_MALL_STAGES > 0 && t >= T - GYM_MALL_STAGES;
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
-            if (!U0Z) bst1(rO, o1, 0, v0);                 // U0Z: the u0 planes stay zero
-            bst1(rO, o1, plane, v1);
+            if (keep) {
+                if (!U0Z) bst1<0>(rO, o1, 0, v0);
+                bst1<0>(rO, o1, plane, v1);
+            } else {
+                if (!U0Z) bst1(rO, o1, 0, v0);             // U0Z: the u0 planes stay zero
+                bst1(rO, o1, plane, v1);
+            }
         }
         gym::rk4(m, n0, n1, n2, n3, v1, pk);
         if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
-            bst2(rX, o2, 0, n0, n1);
-            bst2(rX, o2, WROW, n2, n3);
+            if (keep) {
+                bst2<0>(rX, o2, 0, n0, n1);
+                bst2<0>(rX, o2, WROW, n2, n3);
+            } else {
+                bst2(rX, o2, 0, n0, n1);
+                bst2(rX, o2, WROW, n2, n3);
+            }
         }
     };
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
@@ -700,9 +718,15 @@ __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int 
     const auto rC = rsrc(Cb + (int64_t)t * row);
     if (OUT != OUT_SIGMA) {
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        bst2(rK, o2, 0, k0, k1);
-        bst2(rK, o2, WROW, k2, k3);
-        bst1(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
+        if (GYM_MALL_STAGES > 0 && t < GYM_MALL_STAGES) {
+            bst2<0>(rK, o2, 0, k0, k1);
+            bst2<0>(rK, o2, WROW, k2, k3);
+            bst1<0>(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
+        } else {
+            bst2(rK, o2, 0, k0, k1);
+            bst2(rK, o2, WROW, k2, k3);
+            bst1(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
+        }
     }
     if (OUT != OUT_SOLVER) bst1(rC, o1, plane, s1);
 }
