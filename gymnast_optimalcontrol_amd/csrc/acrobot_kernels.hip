@@ -128,13 +128,13 @@ template <int CP = kNT>
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, CP);
 }
-// GYM_MALL_STAGES: the stages a pass writes last and the next pass reads first (the sweep's lowest stages, the
-// trial's highest knots) are stored with the default cache policy instead of nt, so that part of them is still
-// in the 256 MB Infinity Cache when the next pass starts reading there.  Same-process A/B at 262,144 lanes
-// (profiles/r03/mall/): 0 / 16 / 32 / 64 / 96 / 128 stages -> +0.0 / +0.3 / 0.0 / +0.5..1.2 / 0.0..+0.85 / +0.6%
-// by box, the general (tau1-streaming) path +1.4% at 96; cfg 2 unchanged.  0 turns it off.
+// GYM_MALL_STAGES (measurement variant, default 0 = off): the stages a pass writes last and the next pass reads
+// first (the sweep's lowest stages, the trial's highest knots) stored with the default cache policy instead of nt,
+// so that part of them might still be in the 256 MB Infinity Cache when the next pass starts reading there.  The
+// library-swapping A/B in one process favoured it slightly (profiles/r03/mall/ab_*.log), but bench.py in separate
+// processes on one box, alternating, measured 96 stages 1.7% SLOWER (bench_alternating_processes.log): off.
 #ifndef GYM_MALL_STAGES
-#define GYM_MALL_STAGES 96
+#define GYM_MALL_STAGES 0
 #endif
 
 __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
