@@ -384,8 +384,12 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
 // latency-bound rollout less (cfg 5: 426 -> 412 us, tools/rollout_probe.py; staging the steps in LDS to write
 // whole-trajectory runs was slower, 458 us: LDS traffic shares lgkmcnt with the per-step scalar loads)
 __device__ __forceinline__ void st_nt2(double2* p, double a, double b) {
+#ifdef GYM_TRACK_PLAIN_STORES   // measurement variant: the default cache policy
+    *p = make_double2(a, b);
+#else
     typedef double d2v __attribute__((ext_vector_type(2)));
     __builtin_nontemporal_store(d2v{a, b}, reinterpret_cast<d2v*>(p));
+#endif
 }
 
 // k_track_rollout with each trajectory on a lane pair (gym::rk4_pair): 2B threads, 128 B... of one lane's rows
