@@ -297,7 +297,7 @@ class BatchedNewtonSolver:
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
         self._capture_start(self.capture_lanes or [])
-        self._serial_now = False   # the low-occupancy switch (maybe_compact / _to_serial)
+        self._serial_now = False   # the low-occupancy regime (maybe_compact / _enter_low_occupancy)
         self._run_now = False
         self.batch.flags &= ~_lib.FLAG_SIGMA_STREAM
         if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
@@ -480,13 +480,14 @@ class BatchedNewtonSolver:
 
     def maybe_compact(self, active: int) -> bool:
         """At a host synchronisation (iteration boundary), once at most a quarter of the lanes stay active (a stable
-        population: the count kept at least half its value since the last sync): compact the lanes if they are
-        spread over many wavefronts, and continue a pipelined solve on the serial schedule.  A wavefront runs its
-        whole chains while any of its 64 lanes is active, so late in a hard solve (SURVEY 8(d)'s stress batch:
-        ~22,000 of 262,144 lanes active for hundreds of iterations) every SIMD may still run its four wavefronts for
-        a few lanes each; and with at most one wavefront per SIMD every launch is a latency-bound chain, where the
-        serial schedule runs the post-trial chains once per iteration instead of once per pipeline half.
-        ``active``: this rank's count.  The trigger is rank-local (neither step changes a collective)."""
+        population: the count kept at least half its value since the last sync), enter the low-occupancy regime:
+        move the active lanes to the front (compact) and continue one iteration per launch of the persistent kernel
+        with external retries (_enter_low_occupancy); later, compact again whenever the active lanes are spread over
+        more than twice the wavefronts they need.  A wavefront runs its whole chains while any of its 64 lanes is
+        active, so late in a hard solve (SURVEY 8(d)'s stress batch: ~22,000 of 262,144 lanes active for hundreds of
+        iterations) every SIMD may still run its four wavefronts for a few lanes each; and with at most one
+        wavefront per SIMD every launch is a latency-bound chain.  ``active``: this rank's count.  The trigger is
+        rank-local (neither step changes a collective)."""
         if not self.compact_mode:
             return False
         prev, self._compact_prev = self._compact_prev, int(active)
@@ -499,12 +500,12 @@ class BatchedNewtonSolver:
             if occupied < 2 * (-(-int(active) // 64) + 2) and (self._serial_now or not self.split_waves):
                 if self._serial_now:
                     return False           # already dense, already switched
-                self._to_serial()
+                self._enter_low_occupancy()
                 return True
         self.compact()                     # (entering the persistent kernel's mode: always dense first)
         return True
 
-    def _to_serial(self):
+    def _enter_low_occupancy(self):
         """Continue a pipelined or serial solve one iteration per launch of the four-wavefront persistent kernel
         (k_nt_run2: split Riccati sweep, lane-pair trial chains), its sweep storing sigma1 and the lanes that reject
         trial 1 finished by the serial schedule's parallel candidates and accepted re-run (GYM_FLAG_SIGMA_STREAM);
@@ -524,17 +525,15 @@ class BatchedNewtonSolver:
         state and trajectory buffers, gains, per-lane scalars, histories, per-lane references) and ``lane_order``
         follows, so solve() returns every lane in the caller's order: the results are the uncompacted solve's
         bit for bit (each lane's arithmetic is its own).  Only lanes that change position are moved.
-        ``to_serial`` (the default): a pipelined solve continues on the serial schedule (the next iteration re-runs
-        H0's sweep, which the pipeline had already run: the same values), and the whole batch is one range.  With
-        at most a quarter of the lanes active every wavefront has a SIMD to itself, both schedules are chains of
-        latency-bound launches, and the serial one runs the post-trial chains (sigma1 re-run, candidates, accepted
-        re-run) once per iteration instead of once per half.  Otherwise lanes keep their pipeline half."""
+        ``to_serial`` (the default): the solve then continues in the low-occupancy regime (_enter_low_occupancy;
+        the next iteration re-runs H0's sweep, which the pipeline had already run: the same values), and the whole
+        batch is one range.  Otherwise lanes keep their pipeline half."""
         B, Bp, dev = self.B, self.Bp, self.eng.device
         act = self.status[:B] == _lib.ACTIVE
         perm = torch.arange(Bp, device=dev)
         pipelined = self.pipeline and not self._serial_now and not to_serial
-        if to_serial:   # the serial iteration's sweep then also stores sigma1 (no re-run for rejecting lanes)
-            self._to_serial()
+        if to_serial:
+            self._enter_low_occupancy()
         if pipelined:
             Bh = C.c_int64()
             _lib.check(self.eng.lib.gym_newton_pipeline_split(C.byref(self.batch), C.byref(Bh)),
