@@ -1874,6 +1874,9 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
 #ifndef GYM_RUN2_C
 #define GYM_RUN2_C 2
 #endif
+#ifndef GYM_RUN2_HELPERS
+#define GYM_RUN2_HELPERS 2
+#endif
 constexpr int R2C = GYM_RUN2_C;   // stages per chunk (even)
 constexpr int R2S = 3 * R2C;      // ring slots (the trial uses two chunks of them, the split sweep three)
 constexpr int R2W = 11;           // pairs per lane and slot: sweep x_t (2), u_t, Lin (8); trial x_{t+1} (2), u1_t
@@ -2202,6 +2205,12 @@ __device__ __forceinline__ void run2_trial_main(ring_t ring, int lane, int64_t l
 #ifndef GYM_RUN2_PAIR_VOP3
 #define GYM_RUN2_PAIR_VOP3 1   // three-address Horner steps in the pair trial (acrobot_device.hpp hfma)
 #endif
+#ifndef GYM_RUN2_TRIAL_COPY
+#define GYM_RUN2_TRIAL_COPY 1
+#endif
+#ifndef GYM_RUN2_FETCH0
+#define GYM_RUN2_FETCH0 0   // measurement variant (wrong results): every trial stage re-reads stage 0's K row / cg
+#endif
 // the first Armijo trial's chain on a lane pair (GYM_RUN2_PAIR): two wavefronts share the 64 lanes' RK4 chains,
 // trajectory tl (< 64) of the workgroup on lanes (2q, 2q+1) of wavefront tl / 32 with q = tl % 32; the even lane
 // reduces / rotates th1, the odd lane th2 (gym::rk4_pair, bit-identical to rk4); the ring receives the same rows
@@ -2244,11 +2253,134 @@ __device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_
 #pragma unroll
             for (int j = 0; j < R2C; ++j) {
                 const int t = c * R2C + j, set = cc * R2C + j;
-                step(P[set], (c & 1) * R2C + j);
-                fetch(P[set], uni(min(t + R2PD, T - 1)));
+                if (GYM_RUN2_TRIAL_COPY) {
+                    // the stage's streams moved out of the loading registers first (as run2_sweep_helper): the
+                    // wait is then for this set alone, R2PD stages old, and the set is re-armed at once
+                    TrialStage w = P[set];
+                    in_vgpr2(w.k0); in_vgpr2(w.k1); gym::in_vgpr(w.cg);
+                    fetch(P[set], GYM_RUN2_FETCH0 ? 0 : uni(min(t + R2PD, T - 1)));
+                    step(w, (c & 1) * R2C + j);
+                } else {
+                    step(P[set], (c & 1) * R2C + j);
+                    fetch(P[set], uni(min(t + R2PD, T - 1)));
+                }
             }
             lds_barrier(bw);
         }
+    }
+    lds_barrier(bw);
+}
+
+#ifndef GYM_RUN2_KLOAD
+#define GYM_RUN2_KLOAD 1
+#endif
+#ifndef GYM_RUN2_KLOAD_SGPR
+#define GYM_RUN2_KLOAD_SGPR 1
+#endif
+// GYM_RUN2_KLOAD (with the lane-pair trial and two sweep helpers): the second sweep helper, idle in the trial, becomes
+// the trial's loader.  It reads K row 1 and cg of the stages two chunks ahead from global memory and writes them into
+// an LDS ring three chunks deep ([slot][k0, k1, cg][trajectory]); the two RK4-chain wavefronts read each stage's row
+// from LDS one stage ahead and issue no global loads at all.  With the global loads on the chains the compiler's
+// wait-count placement (loop rotation around the branchy RK4 step) waited for the most recent prefetches once per
+// unrolled body: a load round trip on the chain.  The loader waits for its own loads, off every chain.
+constexpr bool R2KLOAD = GYM_RUN2_KLOAD && R2SPLIT && GYM_RUN2_HELPERS == 2;
+typedef double2 (*kring_t)[3][BLK];
+
+// loader wavefront (GYM_RUN2_KLOAD): chunks 0, 1 before the pass's leading barrier, chunk c + 2 during phase c
+template <bool U0Z>
+__device__ __forceinline__ void run2_trial_kload(kring_t kr, int lane, int64_t l, unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u;
+    const char* Kb = reinterpret_cast<const char*>(R->K1);
+    const char* Cb = reinterpret_cast<const char*>(R->cs);
+    auto fetch = [&](TrialStage& q, int t) {
+        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+        q.k0 = bld2(rK, o2, 0);
+        q.k1 = bld2(rK, o2, WROW);
+        q.cg = bld1(rsrc(Cb + (int64_t)t * row), o1, 0);
+    };
+    auto put = [&](const TrialStage& q, int slot) {
+        kr[slot][0][lane] = q.k0;
+        kr[slot][1][lane] = q.k1;
+        kr[slot][2][lane] = make_double2(q.cg, 0.0);
+    };
+    const int nch = run2_chunks(T);
+    {
+        TrialStage P0[2 * R2C];
+#pragma unroll
+        for (int j = 0; j < 2 * R2C; ++j) fetch(P0[j], uni(min(j, T - 1)));
+#pragma unroll
+        for (int j = 0; j < 2 * R2C; ++j) put(P0[j], j);
+    }
+    TrialStage P[R2C];                     // chunk c + 2's rows, loaded during phase c - 1
+#pragma unroll
+    for (int j = 0; j < R2C; ++j) fetch(P[j], uni(min(2 * R2C + j, T - 1)));
+    lds_barrier(bw);                       // the pass's leading barrier: chunks 0, 1 in the ring
+    int s2 = 2;                            // (c + 2) % 3
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            put(P[j], s2 * R2C + j);
+            fetch(P[j], uni(min((c + 3) * R2C + j, T - 1)));
+        }
+        s2 = s2 == 2 ? 0 : s2 + 1;
+        lds_barrier(bw);
+    }
+    lds_barrier(bw);
+}
+
+// the pair trial's chain (run2_trial_main_pair) fed from the loader's LDS ring: stage t's row is read during stage
+// t - 1 (chunk c + 1's first row during chunk c's last stage: written in phase c - 1)
+template <bool U0Z>
+__device__ __forceinline__ void run2_trial_pair_lds(ring_t ring, kring_t kr, int tl, int64_t l, bool odd, int cb,
+                                                    unsigned long long& bw) {
+    const rargs_t R = run_args();
+    const int T = R->N - 1;
+    const int64_t Bp = R->Bp;
+    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
+    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+    auto get = [&](TrialStage& q, int slot) {
+        q.k0 = kr[slot][0][tl];
+        q.k1 = kr[slot][1][tl];
+        q.cg = kr[slot][2][tl].x;
+    };
+    const gym::PolyRegs pk = gym::poly_vgprs();
+    const int prow = odd ? 1 : 0;
+#if GYM_RUN2_KLOAD_SGPR
+    const Dyn dm = R->m;                   // held in SGPRs across the stage loop: no scalar loads in it, so the
+                                           // LDS reads' lgkmcnt waits are not merged with kernarg loads
+#endif
+    auto step = [&](const TrialStage& q, int slot) {
+        const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
+#if GYM_RUN2_KLOAD_SGPR
+        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
+#else
+        const KArgs ka = kernarg_consts();
+        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, v1, pk);
+#endif
+        double2(*s)[BLK] = ring[slot];
+        s[prow][tl] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+        s[2][tl] = make_double2(v1, 0.0);   // both lanes of the pair: the same value
+    };
+    const int nch = run2_chunks(T);
+    lds_barrier(bw);                       // the loader's chunks 0, 1
+    TrialStage cur;
+    get(cur, 0);
+    int s0 = 0, s1 = 1;                    // c % 3, (c + 1) % 3
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < R2C; ++j) {
+            TrialStage nxt;
+            get(nxt, j + 1 < R2C ? s0 * R2C + j + 1 : s1 * R2C);
+            step(cur, (c & 1) * R2C + j);   // past the end: harmless, not consumed
+            cur = nxt;
+        }
+        s0 = s1;
+        s1 = s1 == 2 ? 0 : s1 + 1;
+        lds_barrier(bw);
     }
     lds_barrier(bw);
 }
@@ -2278,6 +2410,7 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     }
     double J = 0.0;
     const int nch = run2_chunks(T);
+    if (R2KLOAD) lds_barrier(bw);          // the loader's leading barrier
     lds_barrier(bw);                       // the main wavefront's chunk 0
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
@@ -2311,9 +2444,6 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     return J + xcost(R->w.QT, n0, n1, n2, n3, xrT.v);
 }
 
-#ifndef GYM_RUN2_HELPERS
-#define GYM_RUN2_HELPERS 2
-#endif
 constexpr int R2H = GYM_RUN2_HELPERS;   // helper wavefronts: the sweep's stages are dealt to them round-robin
 static_assert(R2H == 1 || R2H == 2, "one or two helper wavefronts");
 // GYM_RUN2_PAIR: a further wavefront (index R2H + 1) joins the main one in the trial, each trajectory's RK4 chain
@@ -2331,6 +2461,7 @@ template <bool U0Z, bool RL>
 __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
     __shared__ double2 ring[R2S][R2W][BLK];
     __shared__ double2 gring[R2SPLIT ? 2 * R2C : 1][3][BLK];   // GYM_RUN2_SPLIT: gain rows, G11, 1/G11
+    __shared__ double2 kring[R2KLOAD ? 3 * R2C : 1][3][BLK];   // GYM_RUN2_KLOAD: the trial's K row 1 / cg
     __shared__ double shJ[BLK];
     __shared__ int shst[BLK];
     const int lane = threadIdx.x & (BLK - 1);
@@ -2376,8 +2507,13 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
         if (wave == 1) {
             shJ[lane] = run2_trial_helper<U0Z, RL>(ring, lane, l, cb, act, run_xr<RL>(run_args(), l),
                                                    run_ur<RL>(run_args(), l), acc[5]);
+        } else if (wave == 2 && R2KLOAD) {
+            run2_trial_kload<U0Z>(kring, lane, l, acc[5]);
         } else if (wave == 2 && R2H == 2) {
             run2_idle(run_args()->N - 1, acc[5]);
+        } else if (R2P && R2KLOAD) {                       // wave 0 and wave R2H + 1: lane pairs, rows from LDS
+            const int tl = (wave == 0 ? 0 : BLK / 2) + (lane >> 1);
+            run2_trial_pair_lds<U0Z>(ring, kring, tl, (int64_t)blockIdx.x * BLK + tl, lane & 1, cb, acc[5]);
         } else if (R2P) {                                  // wave 0 and wave R2H + 1: lane pairs
             const int tl = (wave == 0 ? 0 : BLK / 2) + (lane >> 1);
             run2_trial_main_pair<U0Z>(ring, tl, (int64_t)blockIdx.x * BLK + tl, lane & 1, cb, acc[5]);
