@@ -39,17 +39,31 @@ struct Dyn {
 // one SGPR/literal, so the compiler re-materialises one of them with a v_mov_b64 at every use (16 per
 // RK4 step).  PolyRegs carries those four coefficients; a stage loop takes a VGPR-resident copy
 // (poly_vgprs) once, outside the loop.  Same constants, same operations: the same bits.
+// The other coefficients (s4..s1, c4..c1) are literals in poly_lits() / poly_vgprs(); poly_vgprs_all() holds them
+// in VGPRs too, for a latency-bound loop whose three-address Horner steps (GYM_HORNER_VOP3) need every addend in a
+// VGPR and whose register budget lets them stay there (otherwise each is re-copied from an SGPR at every use).
 struct PolyRegs {
     double s6, s5, c6, c5;
+    double s4, s3, s2, s1, c4, c3, c2, c1;
 };
 __device__ __forceinline__ PolyRegs poly_lits() {
     return PolyRegs{1.58969099521155010221e-10, -2.50507602534068634195e-08, -1.13596475577881948265e-11,
-                    2.08757232129817482790e-09};
+                    2.08757232129817482790e-09,
+                    2.75573137070700676789e-06, -1.98412698298579493134e-04, 8.33333333332248946124e-03,
+                    -1.66666666666666324348e-01,
+                    -2.75573143513906633035e-07, 2.48015872894767294178e-05, -1.38888888888741095749e-03,
+                    4.16666666666666019037e-02};
 }
 __device__ __forceinline__ void in_vgpr(double& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ PolyRegs poly_vgprs() {
     PolyRegs k = poly_lits();
     in_vgpr(k.s6); in_vgpr(k.s5); in_vgpr(k.c6); in_vgpr(k.c5);
+    return k;
+}
+__device__ __forceinline__ PolyRegs poly_vgprs_all() {
+    PolyRegs k = poly_vgprs();
+    in_vgpr(k.s4); in_vgpr(k.s3); in_vgpr(k.s2); in_vgpr(k.s1);
+    in_vgpr(k.c4); in_vgpr(k.c3); in_vgpr(k.c2); in_vgpr(k.c1);
     return k;
 }
 
@@ -75,16 +89,14 @@ __device__ __forceinline__ double hfma(double z, double p, double c) {
 template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ double ksin(double r, double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(r * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.s6, k.s5),
-        2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
-        -1.66666666666666324348e-01), r);
+    return fma(r * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.s6, k.s5), k.s4), k.s3), k.s2),
+        k.s1), r);
 }
 template <bool V3 = GYM_HORNER_VOP3>
 __device__ __forceinline__ double kcos(double z, const PolyRegs& k) {
 #pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
-    return fma(z * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.c6, k.c5),
-        -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
-        4.16666666666666019037e-02), fma(-0.5, z, 1.0));
+    return fma(z * z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, hfma<V3>(z, fma(z, k.c6, k.c5), k.c4), k.c3), k.c2),
+        k.c1), fma(-0.5, z, 1.0));
 }
 
 template <bool V3 = GYM_HORNER_VOP3>
@@ -266,6 +278,66 @@ __device__ __forceinline__ void rk4_pair(const Dyn& m, bool odd, double& x0, dou
     const double n2 = x2 + (m.h * (((a1 + 2.0 * a2) + 2.0 * a3) + a4)) * m.h6;
     const double n3 = x3 + (m.h * (((b1 + 2.0 * b2) + 2.0 * b3) + b4)) * m.h6;
     x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+}
+
+// rk4_pair with every sub-step on the near path (angle addition), no per-sub-step branch: returns false for a
+// lane where a sub-step's increment is outside |d| <= pi/4 (or NaN), whose result must then be discarded and the
+// step re-run by rk4_pair.  Where it returns true the values are rk4_pair's bit for bit (the same near-path code).
+// A lone wavefront issues about one instruction per 4-5 cycles whatever its kind, and each per-sub-step branch
+// costs ~10 of them (compares, exec-mask saves / restores, two conditional jumps); here the three tests fold into
+// two compares and a mask AND per sub-step, and the caller takes one wave-uniform branch per step.
+template <bool V3 = GYM_HORNER_VOP3>
+__device__ __forceinline__ bool rk4_pair_near(const Dyn& m, bool odd, double& x0, double& x1, double& x2, double& x3,
+                                              double tau2, const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
+    constexpr double kPio4 = 0.78539816339744830962;
+    double a1, b1, a2, b2, a3, b3, a4, b4;
+    double t1, u1, t2, u2;
+    const double tho = odd ? x1 : x0;
+    double so, co;
+    fast_sincos<V3>(tho, &so, &co, k);
+    // each lane tests its own joint's increment only: the partner lane tests the other, and one failing lane
+    // sends the whole wavefront (the caller's ballot) through rk4_pair, whose test is per pair
+    bool ok = true;
+    auto sub = [&](double w, double w1, double w2) {   // d = w * (this lane's joint velocity)
+        const double d = w * (odd ? w2 : w1);
+        ok &= fabs(d) <= kPio4;
+        double to, uo;
+        rotate<V3>(so, co, d, to, uo, k);
+        t1 = pair_even(to); u1 = pair_even(uo);
+        t2 = pair_odd(to);  u2 = pair_odd(uo);
+    };
+    const double s1 = pair_even(so), c1 = pair_even(co), s2 = pair_odd(so), c2 = pair_odd(co);
+    accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
+    const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
+    sub(m.h2, x2, x3);
+    accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
+    const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
+    sub(m.h2, y2, y3);
+    accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
+    const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
+    sub(m.h, z2, z3);
+    accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
+    const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
+    const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;
+    const double n2 = x2 + (m.h * (((a1 + 2.0 * a2) + 2.0 * a3) + a4)) * m.h6;
+    const double n3 = x3 + (m.h * (((b1 + 2.0 * b2) + 2.0 * b3) + b4)) * m.h6;
+    x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+    return ok;
+}
+
+// rk4_pair through rk4_pair_near: the branch-free step, re-run with rk4_pair (per-lane sub-step branches) only when
+// a lane of the wavefront needs a far-path sub-step.  Bit-identical to rk4_pair.  Every lane of the wavefront must
+// run it (wave-uniform branch; the pairs' DPP partners are always active).
+template <bool V3 = GYM_HORNER_VOP3>
+__device__ __forceinline__ void rk4_pair_fast(const Dyn& m, bool odd, double& x0, double& x1, double& x2, double& x3,
+                                              double tau2, const PolyRegs& k = poly_lits()) {
+    const double s0 = x0, s1 = x1, s2 = x2, s3 = x3;
+    const bool ok = rk4_pair_near<V3>(m, odd, x0, x1, x2, x3, tau2, k);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0, 0)) {
+        x0 = s0; x1 = s1; x2 = s2; x3 = s3;
+        rk4_pair<V3>(m, odd, x0, x1, x2, x3, tau2, k);
+    }
 }
 
 // Continuous Jacobians (dynamics.py:157-170, 217-226): rows 0,1 of A_c are e3^T, e4^T; B_c[:,0] == 0.

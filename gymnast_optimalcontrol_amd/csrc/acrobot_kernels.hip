@@ -2277,6 +2277,15 @@ __device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_
 #ifndef GYM_RUN2_KLOAD_SGPR
 #define GYM_RUN2_KLOAD_SGPR 1
 #endif
+#ifndef GYM_RUN2_DYN_VGPR
+#define GYM_RUN2_DYN_VGPR 1
+#endif
+#ifndef GYM_RUN2_POLY_ALL
+#define GYM_RUN2_POLY_ALL 1   // every Horner coefficient of the chain's minimax kernels held in VGPRs (gym::poly_vgprs_all)
+#endif
+#ifndef GYM_RUN2_NEAR
+#define GYM_RUN2_NEAR 1   // the chain's RK4 step branch-free on the near path (gym::rk4_pair_fast)
+#endif
 // GYM_RUN2_KLOAD (with the lane-pair trial and two sweep helpers): the second sweep helper, idle in the trial, becomes
 // the trial's loader.  It reads K row 1 and cg of the stages two chunks ahead from global memory and writes them into
 // an LDS ring three chunks deep ([slot][k0, k1, cg][trajectory]); the two RK4-chain wavefronts read each stage's row
@@ -2347,22 +2356,32 @@ __device__ __forceinline__ void run2_trial_pair_lds(ring_t ring, kring_t kr, int
         q.k1 = kr[slot][1][tl];
         q.cg = kr[slot][2][tl].x;
     };
-    const gym::PolyRegs pk = gym::poly_vgprs();
-    const int prow = odd ? 1 : 0;
+    const gym::PolyRegs pk = GYM_RUN2_POLY_ALL ? gym::poly_vgprs_all() : gym::poly_vgprs();
 #if GYM_RUN2_KLOAD_SGPR
-    const Dyn dm = R->m;                   // held in SGPRs across the stage loop: no scalar loads in it, so the
-                                           // LDS reads' lgkmcnt waits are not merged with kernarg loads
+    // the model held in registers across the stage loop: no scalar loads in it, so the LDS reads' lgkmcnt waits are
+    // not merged with kernarg loads (GYM_RUN2_DYN_VGPR: in VGPRs, so that no instruction needs a per-stage copy of a
+    // second scalar operand)
+    Dyn dm = R->m;
+    if (GYM_RUN2_DYN_VGPR) {
+        gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+        gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+        gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
+    }
 #endif
     auto step = [&](const TrialStage& q, int slot) {
         const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
 #if GYM_RUN2_KLOAD_SGPR
-        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
+        if (GYM_RUN2_NEAR)
+            gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
+        else
+            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
 #else
         const KArgs ka = kernarg_consts();
         gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, v1, pk);
 #endif
         double2(*s)[BLK] = ring[slot];
-        s[prow][tl] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
+        s[0][tl] = make_double2(n0, n1);    // both lanes of the pair: the same values, no per-lane select
+        s[1][tl] = make_double2(n2, n3);
         s[2][tl] = make_double2(v1, 0.0);   // both lanes of the pair: the same value
     };
     const int nch = run2_chunks(T);
