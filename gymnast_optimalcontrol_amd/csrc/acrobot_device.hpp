@@ -216,6 +216,50 @@ __device__ __forceinline__ void rk4(const Dyn& m, double& x0, double& x1, double
     x0 = n0; x1 = n1; x2 = n2; x3 = n3;
 }
 
+// rk4 with every sub-step on the near path and no per-sub-step branch (as rk4_pair_near below): false for a lane
+// whose sub-step increments leave |d| <= pi/4 (or are NaN); where true, rk4's values bit for bit.
+__device__ __forceinline__ bool rk4_near(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2,
+                                         const PolyRegs& k = poly_lits()) {
+#pragma clang fp contract(on)   // context-independent bits: FMA contraction inside an expression only
+    constexpr double kPio4 = 0.78539816339744830962;
+    double a1, b1, a2, b2, a3, b3, a4, b4;
+    double s1, c1, s2, c2, t1, u1, t2, u2;
+    bool ok = true;
+    auto sub = [&](double d1, double d2) {
+        ok &= (fabs(d1) <= kPio4) & (fabs(d2) <= kPio4);
+        rotate(s1, c1, d1, t1, u1, k);
+        rotate(s2, c2, d2, t2, u2, k);
+    };
+    fast_sincos(x0, &s1, &c1, k);
+    fast_sincos(x1, &s2, &c2, k);
+    accel_sc(m, s1, c1, s2, c2, x2, x3, tau2, a1, b1);            // k1 = (x2, x3, a1, b1)
+    const double y2 = x2 + m.h2 * a1, y3 = x3 + m.h2 * b1;
+    sub(m.h2 * x2, m.h2 * x3);
+    accel_sc(m, t1, u1, t2, u2, y2, y3, tau2, a2, b2);            // k2 = (y2, y3, a2, b2)
+    const double z2 = x2 + m.h2 * a2, z3 = x3 + m.h2 * b2;
+    sub(m.h2 * y2, m.h2 * y3);
+    accel_sc(m, t1, u1, t2, u2, z2, z3, tau2, a3, b3);            // k3 = (z2, z3, a3, b3)
+    const double v2 = x2 + m.h * a3, v3 = x3 + m.h * b3;
+    sub(m.h * z2, m.h * z3);
+    accel_sc(m, t1, u1, t2, u2, v2, v3, tau2, a4, b4);            // k4 = (v2, v3, a4, b4)
+    const double n0 = x0 + (m.h * (((x2 + 2.0 * y2) + 2.0 * z2) + v2)) * m.h6;
+    const double n1 = x1 + (m.h * (((x3 + 2.0 * y3) + 2.0 * z3) + v3)) * m.h6;
+    const double n2 = x2 + (m.h * (((a1 + 2.0 * a2) + 2.0 * a3) + a4)) * m.h6;
+    const double n3 = x3 + (m.h * (((b1 + 2.0 * b2) + 2.0 * b3) + b4)) * m.h6;
+    x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+    return ok;
+}
+// rk4 through rk4_near, re-run by rk4 only for the lanes that need a far-path sub-step (per lane: no DPP here, so
+// the re-run branch may be divergent).  Bit-identical to rk4.
+__device__ __forceinline__ void rk4_fast(const Dyn& m, double& x0, double& x1, double& x2, double& x3, double tau2,
+                                         const PolyRegs& k = poly_lits()) {
+    const double s0 = x0, s1 = x1, s2 = x2, s3 = x3;
+    if (__builtin_expect(!rk4_near(m, x0, x1, x2, x3, tau2, k), 0)) {
+        x0 = s0; x1 = s1; x2 = s2; x3 = s3;
+        rk4(m, x0, x1, x2, x3, tau2, k);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // One trajectory on a lane pair (lanes 2p, 2p+1 of a wavefront): RK4 with the joint-angle trigonometry split.
 // For a latency-bound rollout (one wavefront per SIMD, each step a dependent chain) the wave's instruction

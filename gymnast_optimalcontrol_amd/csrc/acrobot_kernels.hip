@@ -133,6 +133,9 @@ __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint
 // so that part of them might still be in the 256 MB Infinity Cache when the next pass starts reading there.  The
 // library-swapping A/B in one process favoured it slightly (profiles/r03/mall/ab_*.log), but bench.py in separate
 // processes on one box, alternating, measured 96 stages 1.7% SLOWER (bench_alternating_processes.log): off.
+#ifndef GYM_TRIAL_NEAR
+#define GYM_TRIAL_NEAR 1   // the solver trials' RK4 step on the near path without sub-step branches (gym::rk4_fast)
+#endif
 #ifndef GYM_MALL_STAGES
 #define GYM_MALL_STAGES 0
 #endif
@@ -364,7 +367,10 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
                 bst1(rO, o1, plane, v1);
             }
         }
-        gym::rk4(m, n0, n1, n2, n3, v1, pk);
+        if (GYM_TRIAL_NEAR)
+            gym::rk4_fast(m, n0, n1, n2, n3, v1, pk);
+        else
+            gym::rk4(m, n0, n1, n2, n3, v1, pk);
         if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
             if (keep) {
@@ -2666,6 +2672,9 @@ constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / ex
 #ifndef GYM_TAIL_SPLIT
 #define GYM_TAIL_SPLIT 1
 #endif
+#ifndef GYM_TAIL_NEAR
+#define GYM_TAIL_NEAR 1   // the trials' RK4 chains branch-free on the near path (gym::rk4_pair_fast, as k_nt_run2)
+#endif
 // GYM_TAIL_SPLIT: two wavefronts per tail lane, the sweep's Riccati update split as in k_nt_run2 (Sweep::step_P on
 // wavefront 0, Sweep::step_p, the stores and the next pass's linearisations on wavefront 1, one 64-stage pass
 // behind; linearisations triple-buffered, the gain rows double-buffered); the trials stay on wavefront 0
@@ -2901,7 +2910,9 @@ __device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, i
             if (!U0Z) bst1(rO, v1o, 0, v0);
             bst1(rO, v1o, splane, u1);
         }
-        if (PAIR)
+        if (PAIR && GYM_TAIL_NEAR)
+            gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
+        else if (PAIR)
             gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
         else
             gym::rk4(m, n0, n1, n2, n3, u1, pk);
@@ -2941,7 +2952,10 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
                 const double y = trial_u1(k0, k1, q[4], n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
                 const double ysig = __builtin_fma(dg, q[5], y);             // trial_u1_sig's value
                 const double u1 = c == 0 ? y : ysig;
-                gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
+                if (GYM_TAIL_NEAR)
+                    gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
+                else
+                    gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
                 double2* r = ring[cc & 1][j][tc];
                 if (odd) r[1] = make_double2(n2, n3);
                 else { r[0] = make_double2(n0, n1); r[2] = make_double2(u1, 0.0); }

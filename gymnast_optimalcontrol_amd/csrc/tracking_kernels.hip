@@ -18,6 +18,9 @@
 #define GYM_HORNER_VOP3 1   // three-address Horner steps (acrobot_device.hpp): no per-step constant copies
 #endif
 #include "acrobot_device.hpp"
+#ifndef GYM_TRACK_NEAR
+#define GYM_TRACK_NEAR 1   // the pair rollout's RK4 step branch-free on the near path (gym::rk4_pair_fast)
+#endif
 #include "gymnast_acrobot.h"
 
 using gym::Dyn;
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
 #pragma unroll
     for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
     f[0] = u_ff[0]; f[1] = u_ff[1];
-    const gym::PolyRegs pk = gym::poly_vgprs();
+    const gym::PolyRegs pk = GYM_TRACK_NEAR ? gym::poly_vgprs_all() : gym::poly_vgprs();
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
         const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
@@ -430,7 +433,10 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
             f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
         }
         if (!odd) st_nt2(ul + t, v0, v1);
-        gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
+        if (GYM_TRACK_NEAR)
+            gym::rk4_pair_fast(m, odd, n0, n1, n2, n3, v1, pk);
+        else
+            gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
         if (odd) st_nt2(xl + 2 * (t + 1), n2, n3);
         else st_nt2(xl + 2 * (t + 1), n0, n1);
     }
