@@ -1908,6 +1908,9 @@ constexpr int R2RD = R2SPLIT ? 3 : 2;   // helper ring depth in chunks (sweep)
 // take ~1 us: with one stage of prefetch both passes ran at the load latency (~2,400 cycles per stage measured,
 // whatever the instruction count, tools/run2_trace.py).
 constexpr int R2PD = GYM_RUN2_PD;
+#ifndef GYM_RUN2_SWEEP_VGPR
+#define GYM_RUN2_SWEEP_VGPR 1   // the sweep roles' constants held in VGPRs across their stage loops
+#endif
 #ifndef GYM_RUN2_DYN_SGPR
 #define GYM_RUN2_DYN_SGPR 0   // measurement variant: the trial's model coefficients held in SGPRs
 #endif
@@ -1973,7 +1976,20 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
     const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
     // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them); per-lane
     // references (RL): the lane's own rows
+#if GYM_RUN2_SWEEP_VGPR
+    // the model, the weights stage_lin reads and every Horner coefficient held in VGPRs across the stage loop: no
+    // per-stage kernel-argument loads (and their lgkmcnt(0) waits) and no per-use copies of scalar operands
+    const gym::PolyRegs pk = gym::poly_vgprs_all();
+    Dyn dm = R->m;
+    KW wv = R->w;
+    gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+    gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+    gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
+    gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
+    gym::in_vgpr(wv.G00); gym::in_vgpr(wv.twoR1);
+#else
     const gym::PolyRegs pk = gym::poly_vgprs();
+#endif
     auto fetch = [&](SweepStage& q, int t) {
         const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)t * row);
         q.xa = bld2(rX, o2, 0);
@@ -1982,11 +1998,18 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
         q.u1 = bld1(rU, o1, plane);
     };
     auto produce = [&](const SweepStage& q, int t, int slot) {
+#if GYM_RUN2_SWEEP_VGPR
+        const gym::Jac J = gym::jacobian(dm, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
+        const Row<4> xrt = ref_row<4, RL>(xr, t);
+        const Row<2> urt = ref_row<2, RL>(ur, t);
+        const Lin L = stage_lin<U0Z>(dm, wv, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
+#else
         const KArgs ka = kernarg_consts();
         const gym::Jac J = gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
         const Row<4> xrt = ref_row<4, RL>(xr, t);
         const Row<2> urt = ref_row<2, RL>(ur, t);
         const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
+#endif
         double2(*s)[BLK] = ring[slot];
         s[0][lane] = q.xa;                          s[1][lane] = q.xb;
         s[2][lane] = make_double2(q.u0, q.u1);      s[3][lane] = make_double2(L.A20, L.A21);
@@ -2076,6 +2099,12 @@ __device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int 
     const double2* x = R->x[cb];
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, R->Bp)], x[wix(T, 1, 2, l, R->Bp)], run_xr<RL>(R, l) + 4 * T);
     const int nch = run2_chunks(T);
+#if GYM_RUN2_SWEEP_VGPR
+    KW wv = R->w;                          // step_P's weights and dt in VGPRs: no per-stage kernel-argument loads
+    double dtv = R->m.h;
+    gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
+    gym::in_vgpr(wv.twoR1); gym::in_vgpr(dtv);
+#endif
     lds_barrier(bw);                       // the helpers' chunk 0
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
@@ -2085,11 +2114,18 @@ __device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int 
                 const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
                 const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
                 const double2 bd = s[7][lane];
+#if GYM_RUN2_SWEEP_VGPR
+                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
+                            0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dtv};      // q, r: the vector half's
+                double k0, k1, k2, k3, G11, iG;
+                S.step_P(wv, L, k0, k1, k2, k3, G11, iG);
+#else
                 const KArgs ka = kernarg_consts();
                 const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
                             0.0, 0.0, 0.0, 0.0, 0.0, 0.0, ka.m.h};   // q, r: the vector half's
                 double k0, k1, k2, k3, G11, iG;
                 S.step_P(ka.w, L, k0, k1, k2, k3, G11, iG);
+#endif
                 double2(*g)[BLK] = gring[(c & 1) * R2C + j];
                 g[0][lane] = make_double2(k0, k1);
                 g[1][lane] = make_double2(k2, k3);
@@ -2119,6 +2155,11 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
     const double2* x = R->x[cb];
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], run_xr<RL>(R, l) + 4 * T);
     const int nch = run2_chunks(T);
+#if GYM_RUN2_SWEEP_VGPR
+    KW wv = R->w;                          // step_p's weights and dt in VGPRs: no per-stage kernel-argument loads
+    double dtv = R->m.h;
+    gym::in_vgpr(wv.iG00); gym::in_vgpr(dtv);
+#endif
     lds_barrier(bw);                       // the helpers' chunk 0
     lds_barrier(bw);                       // the main wavefront's chunk 0
     for (int c = 0; c < nch; ++c) {
@@ -2132,11 +2173,18 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
                 const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
                 const double2(*g)[BLK] = gring[(c & 1) * R2C + j];
                 const double2 ka01 = g[0][lane], ka23 = g[1][lane], gi = g[2][lane];
+#if GYM_RUN2_SWEEP_VGPR
+                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
+                            qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, dtv};
+                double s0, s1;
+                S.step_p<U0Z>(wv, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
+#else
                 const KArgs ka = kernarg_consts();
                 const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
                             qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
                 double s0, s1;
                 S.step_p<U0Z>(ka.w, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
+#endif
                 if (act) {
                     if (ext)   // external retries: sigma1 stored too (the candidates read it; no re-run)
                         store_stage<OUT_ALL>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
