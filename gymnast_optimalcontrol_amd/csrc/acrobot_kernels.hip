@@ -2720,6 +2720,9 @@ constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / ex
 #ifndef GYM_TAIL_SPLIT
 #define GYM_TAIL_SPLIT 1
 #endif
+#ifndef GYM_TAIL_SWEEP_VGPR
+#define GYM_TAIL_SWEEP_VGPR 1   // the split tail sweep's weights held in VGPRs across its stage loops
+#endif
 #ifndef GYM_TAIL_NEAR
 #define GYM_TAIL_NEAR 1   // the trials' RK4 chains branch-free on the near path (gym::rk4_pair_fast, as k_nt_run2)
 #endif
@@ -2850,6 +2853,11 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
             tst[t * TL_TST + 6] = u0;
         }
     };
+#if GYM_TAIL_SWEEP_VGPR
+    KW wv = R->w;                          // the Riccati halves' weights in VGPRs: no per-stage kernel-argument loads
+    gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
+    gym::in_vgpr(wv.twoR1); gym::in_vgpr(wv.iG00);
+#endif
     if (wave == 1) linearise(0);
     __syncthreads();
     for (int j = 0; j <= np; ++j) {
@@ -2861,11 +2869,15 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                 double* G = gk2 + (j & 1) * TL_STAGES * TL_GK;
                 for (int i = 0; i < n; ++i) {
                     const double* s = L3 + i * TL_PITCH;
-                    const KArgs ka = kernarg_consts();
+#if GYM_TAIL_SWEEP_VGPR
+                    const KW& kw = wv;
+#else
+                    const KW kw = kernarg_consts().w;
+#endif
                     const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
                                 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dt};   // q, r: the vector half's
                     double k0, k1, k2, k3, G11, iG;
-                    S.step_P(ka.w, L, k0, k1, k2, k3, G11, iG);
+                    S.step_P(kw, L, k0, k1, k2, k3, G11, iG);
                     if (lane == 0) {
                         double* g = G + i * TL_GK;
                         g[0] = k0; g[1] = k1; g[2] = k2; g[3] = k3; g[4] = G11; g[5] = iG;
@@ -2883,11 +2895,15 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                     const double* s = L3 + i * TL_PITCH;
                     const double* g = G + i * TL_GK;
                     const double k0 = g[0], k1 = g[1], k2 = g[2], k3 = g[3];
-                    const KArgs ka = kernarg_consts();
+#if GYM_TAIL_SWEEP_VGPR
+                    const KW& kw = wv;
+#else
+                    const KW kw = kernarg_consts().w;
+#endif
                     const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
                                 s[10], s[11], s[12], s[13], s[14], s[15], dt};
                     double s0, s1;
-                    S.step_p<U0Z>(ka.w, L, k0, k1, k2, k3, g[4], g[5], s0, s1);
+                    S.step_p<U0Z>(kw, L, k0, k1, k2, k3, g[4], g[5], s0, s1);
                     if (lane == 0) {
                         const int ts = tb - i;
                         const double2 xa = make_double2(s[16], s[17]), xb = make_double2(s[18], s[19]);
