@@ -18,6 +18,9 @@
 #define GYM_HORNER_VOP3 1   // three-address Horner steps (acrobot_device.hpp): no per-step constant copies
 #endif
 #include "acrobot_device.hpp"
+#ifndef GYM_TRACK_DYN_VGPR
+#define GYM_TRACK_DYN_VGPR 1
+#endif
 #ifndef GYM_TRACK_NEAR
 #define GYM_TRACK_NEAR 1   // the pair rollout's RK4 step branch-free on the near path (gym::rk4_pair_fast)
 #endif
@@ -420,6 +423,12 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
     for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
     f[0] = u_ff[0]; f[1] = u_ff[1];
     const gym::PolyRegs pk = GYM_TRACK_NEAR ? gym::poly_vgprs_all() : gym::poly_vgprs();
+    Dyn dm = m;                            // GYM_TRACK_DYN_VGPR: the model in VGPRs across the step loop
+    if (GYM_TRACK_DYN_VGPR) {
+        gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+        gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+        gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
+    }
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
         const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
@@ -434,7 +443,7 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
         }
         if (!odd) st_nt2(ul + t, v0, v1);
         if (GYM_TRACK_NEAR)
-            gym::rk4_pair_fast(m, odd, n0, n1, n2, n3, v1, pk);
+            gym::rk4_pair_fast(dm, odd, n0, n1, n2, n3, v1, pk);
         else
             gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
         if (odd) st_nt2(xl + 2 * (t + 1), n2, n3);
