@@ -2723,6 +2723,9 @@ constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / ex
 #ifndef GYM_TAIL_SWEEP_VGPR
 #define GYM_TAIL_SWEEP_VGPR 1   // the split tail sweep's weights held in VGPRs across its stage loops
 #endif
+#ifndef GYM_TAIL_CHAIN_VGPR
+#define GYM_TAIL_CHAIN_VGPR 1
+#endif
 #ifndef GYM_TAIL_NEAR
 #define GYM_TAIL_NEAR 1   // the trials' RK4 chains branch-free on the near path (gym::rk4_pair_fast, as k_nt_run2)
 #endif
@@ -3001,9 +3004,18 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
     const double dg = g - R->a.gamma0;
     const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
     double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+#if GYM_TAIL_CHAIN_VGPR
+    // every Horner coefficient and the model in VGPRs across the chain's loop (as k_nt_run2's trial chain)
+    const gym::PolyRegs pk = gym::poly_vgprs_all();
+    Dyn m = kernarg_consts().m;
+    gym::in_vgpr(m.b); gym::in_vgpr(m.d); gym::in_vgpr(m.a2b); gym::in_vgpr(m.bb); gym::in_vgpr(m.dad);
+    gym::in_vgpr(m.g1); gym::in_vgpr(m.g2); gym::in_vgpr(m.f1); gym::in_vgpr(m.f2); gym::in_vgpr(m.h);
+    gym::in_vgpr(m.h2); gym::in_vgpr(m.h6);
+#else
     const gym::PolyRegs pk = gym::poly_vgprs();
     const KArgs ka = kernarg_consts();
     const Dyn m = ka.m;
+#endif
     const int nch = (T + TL_RC - 1) / TL_RC;
     const int tc = c < BLK / 2 ? c : 0;
     for (int cc = 0; cc < nch; ++cc) {
