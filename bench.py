@@ -201,7 +201,7 @@ class NewtonLeg:
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
             schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
-            split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes,
+            split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes, world_size=self.world,
             compact=None if a.compact == "auto" else a.compact == "on")
         if timing:
             self.solver.enable_timing()

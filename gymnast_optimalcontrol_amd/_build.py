@@ -25,11 +25,14 @@ ARCH = os.environ.get("GYM_OFFLOAD_ARCH", "gfx950")
 BUILD_ID_TAG = b"gym-build-id:"      # marker in front of the id string inside the library's .rodata
 
 
-def source_hash() -> str:
-    """Build id of the tree: sha256 over the kernel sources and the ABI header (names and contents), 16 hex
-    digits.  The library embeds the id it was compiled from (gym_build_id); _lib.load refuses a mismatch, so a
-    stale libgymnast_acrobot.so that travelled with the tree can never run silently against newer sources."""
+def source_hash(defines=(), arch: str | None = None) -> str:
+    """Build id: sha256 over the kernel sources and the ABI header (names and contents), the offload architecture
+    and the sorted extra preprocessor defines, 16 hex digits.  The library embeds the id it was compiled from
+    (gym_build_id); _lib.load refuses anything but the canonical id (no defines, GYM_OFFLOAD_ARCH), so neither a
+    stale libgymnast_acrobot.so that travelled with the tree nor an A/B variant compiled with extra defines can run
+    silently as the product."""
     h = hashlib.sha256()
+    h.update(f"arch={arch or ARCH}\0defines={' '.join(sorted(defines))}\0".encode())
     for p in sorted(DEPS):
         h.update(os.path.basename(p).encode() + b"\0")
         with open(p, "rb") as f:
@@ -71,7 +74,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
         return LIB_PATH
     tmp = target + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           f"-DGYM_BUILD_ID=\"{source_hash()}\"", *[f"-D{d}" for d in defines], "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
+           f"-DGYM_BUILD_ID=\"{source_hash(defines)}\"", *[f"-D{d}" for d in defines], "-I", INCLUDE, "-I", CSRC, *SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -21,19 +21,28 @@ STATE_SYMBOLS = ("theta1", "theta2", "theta1_dot", "theta2_dot")
 INPUT_SYMBOLS = ("tau1", "tau2")
 
 
-def _mechanics(sp, s):
-    """M, C, G, F of the double pendulum with joint friction (dynamics.py:63-90), from the symbol table s."""
+def _entries(sp, s):
+    """The reference's module-level scalar entries M11 .. M22, C11 .. C22, G1, G2 (dynamics.py:64-83), unsimplified
+    as the reference leaves them (M and Gvec simplify them entry by entry)."""
     c2, s2 = sp.cos(s["theta2"]), sp.sin(s["theta2"])
     h = s["l1"] * s["lc2"] * s["m2"]                       # the coupling coefficient m2 l1 lc2
     d = s["I2"] + s["m2"] * s["lc2"] ** 2
     m_off = d + h * c2
-    m_11 = s["I1"] + s["m1"] * s["lc1"] ** 2 + s["m2"] * (s["l1"] ** 2 + s["lc2"] ** 2) + s["I2"] + 2 * h * c2
-    Mm = sp.Matrix([[sp.simplify(m_11), sp.simplify(m_off)], [sp.simplify(m_off), sp.simplify(d)]])
     w1, w2 = s["theta1_dot"], s["theta2_dot"]
-    Cm = sp.Matrix([[-h * s2 * w2, -h * s2 * (w1 + w2)], [h * s2 * w1, 0]])
     s1, s12 = sp.sin(s["theta1"]), sp.sin(s["theta1"] + s["theta2"])
-    Gv = sp.Matrix([[sp.simplify(s["g"] * (s["m1"] * s["lc1"] + s["m2"] * s["l1"]) * s1 + s["g"] * s["m2"] * s["lc2"] * s12)],
-                    [sp.simplify(s["g"] * s["m2"] * s["lc2"] * s12)]])
+    g2 = s["g"] * s["m2"] * s["lc2"] * s12
+    return {"M11": s["I1"] + s["m1"] * s["lc1"] ** 2 + s["m2"] * (s["l1"] ** 2 + s["lc2"] ** 2) + s["I2"] + 2 * h * c2,
+            "M12": m_off, "M21": m_off, "M22": d,
+            "C11": -h * s2 * w2, "C12": -h * s2 * (w1 + w2), "C21": h * s2 * w1, "C22": 0,
+            "G1": s["g"] * (s["m1"] * s["lc1"] + s["m2"] * s["l1"]) * s1 + g2, "G2": g2}
+
+
+def _mechanics(sp, s):
+    """M, C, G, F of the double pendulum with joint friction (dynamics.py:63-90), from the symbol table s."""
+    e = _entries(sp, s)
+    Mm = sp.Matrix([[sp.simplify(e["M11"]), sp.simplify(e["M12"])], [sp.simplify(e["M21"]), sp.simplify(e["M22"])]])
+    Cm = sp.Matrix([[e["C11"], e["C12"]], [e["C21"], e["C22"]]])
+    Gv = sp.Matrix([[sp.simplify(e["G1"])], [sp.simplify(e["G2"])]])
     Fm = sp.diag(s["f1"], s["f2"])
     return Mm, Cm, Gv, Fm
 
@@ -46,6 +55,7 @@ def model() -> dict:
     s = {n: sp.Symbol(n) for n in PARAM_SYMBOLS + STATE_SYMBOLS + INPUT_SYMBOLS}
     Mm, Cm, Gv, Fm = _mechanics(sp, s)
     out = dict(s)
+    out.update(_entries(sp, s))
     out.update(M=Mm, C=Cm, Gvec=Gv, F=Fm)
     p1 = PARAM_SETS[1]
     out.update(M_num=Mm.subs(p1), C_num=Cm.subs(p1), G_num=Gv.subs(p1), F_num=Fm.subs(p1))
@@ -92,6 +102,7 @@ def set_params(version_num):
 
 
 NAMES = (PARAM_SYMBOLS + STATE_SYMBOLS + INPUT_SYMBOLS +
+         ("M11", "M12", "M21", "M22", "C11", "C12", "C21", "C22", "G1", "G2") +
          ("M", "C", "Gvec", "F", "M_num", "C_num", "G_num", "F_num", "q_syms", "qdot_syms", "all_syms", "u_syms",
           "x_syms", "tau_vec", "qdot_vec", "RHS_expr", "qddot_expr", "f_expr", "M_func", "RHS_func", "A_expr",
           "B_expr", "M_sym", "C_sym", "G_sym", "F_sym", "q_vec", "x_vec", "u_vec", "tau_acrobot", "RHS_sym",

@@ -2716,7 +2716,9 @@ __device__ __forceinline__ targs_t tail_args() {
 // The trials' per-stage inputs are staged in LDS by the sweep (K row 1, cg, sigma1 and u0: 8 doubles per stage), so
 // the trial loop issues no global loads: its scratch stores are never waited on (the GFX9 vmcnt counts both)
 constexpr int TL_TST = 8;
-constexpr int TL_MAX_T = 640;    // T * 64 B of staging + the linearisation / exchange areas within 56 KiB of LDS
+constexpr int TL_MAX_T = 640;    // T * 64 B of trial staging (40 KiB) + the linearisation / gain / exchange areas: tail_lds_bytes(T),
+                                 // ~72 KiB at T = 500, ~87 KiB at T = 640: above the 64 KiB default, so every launch raises
+                                 // the kernel's dynamic-LDS limit (gfx950: 160 KiB); gym_newton_tail_lds reports both
 #ifndef GYM_TAIL_SPLIT
 #define GYM_TAIL_SPLIT 1
 #endif
@@ -3853,6 +3855,19 @@ int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t*
     return 0;
 }
 
+int gym_newton_tail_lds(int32_t N, int64_t* bytes_out, int64_t* limit_out) {
+    if (!bytes_out || N < 2 || N - 1 > TL_MAX_T) return GYM_EINVAL;
+    *bytes_out = (int64_t)tail_lds_bytes(N - 1);
+    if (limit_out) {   // the current device's opt-in LDS per workgroup
+        int dev = 0, lim = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&lim, hipDeviceAttributeSharedMemPerBlockOptin, dev);
+        if (e != hipSuccess) return (int)e;
+        *limit_out = lim;
+    }
+    return 0;
+}
+
 int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                     const int32_t* lanes, int32_t n_lanes, double* scratch, int64_t scratch_doubles, int32_t k0,
                     int32_t k1, void* s) {
@@ -4041,22 +4056,30 @@ int gym_timing_destroy(gym_timing* t) {
 
 int gym_timing_collect(gym_timing* t) {
     if (!t) return GYM_EINVAL;
+    // every recorded pair is read first and committed only when all of them succeeded: on an error (e.g.
+    // hipErrorNotReady, the stream not synchronised) the record is unchanged and a later collect counts each pair once
+    double ms_add[GYM_NK] = {};
+    int n_add[GYM_NK] = {};
     for (int i = 0; i < GYM_NK; ++i) {
         if (!(t->pending & (1 << i))) continue;
         float ms = 0.f;
         hipError_t r = hipEventElapsedTime(&ms, (hipEvent_t)t->ev[2 * i], (hipEvent_t)t->ev[2 * i + 1]);
         if (r != hipSuccess) return (int)r;
-        t->ms[i] += ms;
-        t->launches[i] += 1;
+        ms_add[i] += ms;
+        n_add[i] += 1;
     }
-    t->pending = 0;
     for (int j = 0; j < t->pool_used; ++j) {
         float ms = 0.f;
         hipError_t r = hipEventElapsedTime(&ms, (hipEvent_t)t->pool_ev[2 * j], (hipEvent_t)t->pool_ev[2 * j + 1]);
         if (r != hipSuccess) return (int)r;
-        t->ms[t->pool_kind[j]] += ms;
-        t->launches[t->pool_kind[j]] += 1;
+        ms_add[t->pool_kind[j]] += ms;
+        n_add[t->pool_kind[j]] += 1;
     }
+    for (int i = 0; i < GYM_NK; ++i) {
+        t->ms[i] += ms_add[i];
+        t->launches[i] += n_add[i];
+    }
+    t->pending = 0;
     t->pool_used = 0;
     return 0;
 }

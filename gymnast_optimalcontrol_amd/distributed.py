@@ -146,6 +146,7 @@ def solve_sharded(x0_all, x_ref, u_ref, max_iters, engine=None, keep_stats: bool
         x_ref, u_ref = x_ref[lo:hi], u_ref[lo:hi]
     eng = engine or AcrobotEngine()
     solver_kw.setdefault("schedule_lanes", schedule_lanes(total, world))
+    solver_kw.setdefault("world_size", world)
     solver = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **solver_kw)
     x0_loc = x0_all[lo:hi] if isinstance(x0_all, torch.Tensor) else np.asarray(x0_all)[lo:hi]
     res = solver.solve(x0_loc, max_iters, reduce_stats=make_reduce_stats(force=force_collectives),

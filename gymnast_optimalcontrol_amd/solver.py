@@ -101,7 +101,7 @@ class BatchedNewtonSolver:
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
                  capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
                  capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128,
-                 compact: bool | None = None):
+                 compact: bool | None = None, world_size: int = 1):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -214,13 +214,19 @@ class BatchedNewtonSolver:
         self.capture_sigma = tuple(sorted({int(i) for i in (capture_sigma or ())}))
         # straggler tail (serial / pipelined schedules; needs the full state store, whole-iteration launches: no
         # trajectory capture, at most 64 Armijo trials): switch once the global active count is <= tail_lanes.
-        # Default: on with the automatic schedule choice; a caller that picks a schedule gets it pure
+        # Default: on with the automatic schedule choice, TAIL_LANES_PER_CU per CU of every rank (``world_size``:
+        # the ranks the statistics are all-reduced over, so the switch comes at the same per-GPU occupancy at any
+        # world size); a caller that picks a schedule gets it pure
         if tail_lanes is None:
-            tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count
-                          if auto_schedule else 0)
-        need = C.c_int64()   # the tail kernel's limits: at most 64 trials, horizons up to its LDS staging
+            tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count *
+                          max(int(world_size), 1) if auto_schedule else 0)
+        # the tail kernel's limits: at most 64 trials, horizons up to its LDS staging, and that LDS within the
+        # device's opt-in limit (checked here, so a device with less LDS turns the tail off instead of failing mid-solve)
+        need, lds, lds_max = C.c_int64(), C.c_int64(), C.c_int64()
         tail_ok = (not self.persistent and not self.checkpoint and self.capture_lanes is None and
-                   engine.lib.gym_newton_tail_scratch(self.N, 1, int(max_ls), C.byref(need)) == 0)
+                   engine.lib.gym_newton_tail_scratch(self.N, 1, int(max_ls), C.byref(need)) == 0 and
+                   engine.lib.gym_newton_tail_lds(self.N, C.byref(lds), C.byref(lds_max)) == 0 and
+                   lds.value <= lds_max.value)
         self.tail_lanes = int(tail_lanes) if tail_ok else 0
         self.tail_chunk = max(int(tail_chunk), 1)
         # lane compaction (serial / pipelined schedules, solve(); see maybe_compact): default on with the automatic
@@ -258,6 +264,7 @@ class BatchedNewtonSolver:
     def reset_timing(self):
         self.launches = {"phase": 0, "run": 0, "tail": 0, "iteration": 0}
         if self.timing is not None:
+            torch.cuda.synchronize(self.eng.device)   # collect_timing reads completed event pairs only
             self.collect_timing()       # drains the pool (pairs of launches before the reset)
             for i in range(len(_lib.KERNEL_KINDS)):
                 self.timing.ms[i] = 0.0
@@ -738,6 +745,7 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
     (a lane stops inside a launch when it finishes; the launch ends with its last lane); the statistics are
     all-reduced and read after each launch, and the loop stops when no lane of any rank is active."""
     log = []
+    k_switch = k
     its0 = int(solver.n_iter[:solver.B].sum().item())
     solver._its_tail_start = its0
     while k < max_iters:
@@ -757,6 +765,11 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
         if host[0] == 0:
             break
     solver.tail_lane_its = int(solver.n_iter[:solver.B].sum().item()) - its0
+    # a launch runs up to tail_chunk iterations but ends with its last lane: report the last iteration a lane ran,
+    # not the end of the chunk.  Sharded (reduce_stats): the chunk end, identical on every rank, as the lock-step loop
+    # reports its global count (a rank-local maximum would differ between ranks)
+    if reduce_stats is None and solver.B:
+        solver.k = max(k_switch, min(solver.k, int(solver.n_iter[:solver.B].max().item())))
     return log
 
 

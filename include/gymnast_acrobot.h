@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 11
+#define GYM_ABI_VERSION 12
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -262,6 +262,10 @@ int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* 
                     int32_t k1, void* stream);
 /* [host] Scratch doubles gym_newton_tail needs for n_lanes lanes (candidate trajectories of every trial). */
 int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t* doubles_out);
+/* LDS per workgroup the tail kernel needs at horizon N (*bytes_out; ~72 KiB at N = 501), and, if limit_out is not
+ * NULL, the current device's opt-in limit (hipDeviceAttributeSharedMemPerBlockOptin; a HIP error code if the
+ * device cannot be queried).  A caller turns the tail off up front when bytes > limit (solver.py tail_ok). */
+int gym_newton_tail_lds(int32_t N, int64_t* bytes_out, int64_t* limit_out);
 /* After k_done iterations: ACTIVE lanes -> GYM_MAX_ITERS; gather each lane's result buffer into lane-major
  * x_out (B,N,4), u_out (B,T,2), K_out (B,T,2,4) and sigma_out (B,T,2) of the lane's last iteration
  * (sigma0 recomputed from that iteration's u0).  Any output may be NULL.  With GYM_FLAG_X_CKPT the result

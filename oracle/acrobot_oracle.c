@@ -195,11 +195,25 @@ double orc_forward(const orc_model* m, const orc_cost* c, const double* x, const
     return J + term_cost(c, xn + 4 * (N - 1), xr + 4 * (N - 1));
 }
 
+/* Optional per-iteration record of one lane (NULL pointers: not recorded).  Row k holds iteration k:
+ * cost after the iteration (the reference's history['cost'][k+1]; the unchanged cost on an LS failure),
+ * max|sigma| of its sweep (history['sigma_norm'][k]), the Armijo trials it evaluated, and the tightest
+ * Armijo test of the iteration: min over its trials of |J_new - (J + c gamma dJ)| / max(|J|, tiny) --
+ * how far the closest accept / reject call was from a tie (a rounding-level value flags a decision that
+ * another restatement may take the other way). */
+typedef struct {
+    int hist_len;
+    double* cost;
+    double* smax;
+    int32_t* trials;
+    double* margin;
+} orc_hist;
+
 /* Newton / Armijo for one lane (trajectory_generation.py:298-398). Work buffers owned here. */
 static void solve_lane(const orc_model* m, const orc_cost* c, const double* x0, const double* xr, const double* ur,
                        int N, int max_iters, double tol, double beta, double cc, double gamma0, int max_ls,
                        double* x, double* u, double* K1, double* sig, int32_t* n_iter, int32_t* status,
-                       double* cost, int32_t* n_roll) {
+                       double* cost, int32_t* n_roll, const orc_hist* h, int64_t lane) {
     const int T = N - 1;
     double* xn = (double*)malloc(sizeof(double) * 4 * N);
     double* un = (double*)malloc(sizeof(double) * 2 * T);
@@ -211,13 +225,23 @@ static void solve_lane(const orc_model* m, const orc_cost* c, const double* x0, 
     for (int k = 0; k < max_iters && st == ORC_ACTIVE; k++) {
         double smax;
         double dJ = orc_backward(m, c, x, u, xr, ur, N, K1, sig, &smax);
-        double g = gamma0, Jn = 0.0;
-        int ok = 0;
-        for (int i = 0; i < max_ls; i++) {
+        double g = gamma0, Jn = 0.0, tight = INFINITY;
+        int ok = 0, i;
+        for (i = 0; i < max_ls; i++) {
             Jn = orc_forward(m, c, x, u, K1, sig, g, xr, ur, N, xn, un);
             nr++;
-            if (Jn < J + cc * g * dJ) { ok = 1; break; }
+            double rhs = J + cc * g * dJ;
+            double mg = fabs(Jn - rhs) / fmax(fabs(J), 1e-300);
+            if (mg < tight || mg != mg) tight = mg;
+            if (Jn < rhs) { ok = 1; break; }
             g *= beta;
+        }
+        if (h && k < h->hist_len) {
+            int64_t o = lane * h->hist_len + k;
+            if (h->cost) h->cost[o] = ok ? Jn : J;
+            if (h->smax) h->smax[o] = smax;
+            if (h->trials) h->trials[o] = ok ? i + 1 : max_ls;
+            if (h->margin) h->margin[o] = tight;
         }
         it++;
         if (!ok) { st = ORC_LS_FAILED; break; }
@@ -231,16 +255,35 @@ static void solve_lane(const orc_model* m, const orc_cost* c, const double* x0, 
     free(xn); free(un);
 }
 
+static void solve_batch(const orc_model* m, const orc_cost* c, const double* x0, const double* xr, const double* ur,
+                        int64_t B, int N, int max_iters, double tol, double beta, double cc, double gamma0, int max_ls,
+                        double* x, double* u, double* K1, double* sig, int32_t* n_iter, int32_t* status, double* cost,
+                        int32_t* n_roll, const orc_hist* h) {
+    const int64_t T = N - 1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t l = 0; l < B; l++)
+        solve_lane(m, c, x0 + 4 * l, xr, ur, N, max_iters, tol, beta, cc, gamma0, max_ls, x + 4 * N * l,
+                   u + 2 * T * l, K1 + 4 * T * l, sig + 2 * T * l, n_iter + l, status + l, cost + l, n_roll + l, h, l);
+}
+
 /* Batched entry: lanes are independent; x0 (B,4) -> x (B,N,4), u (B,T,2), K1 (B,T,4), sig (B,T,2). */
 void orc_newton_solve(const orc_model* m, const orc_cost* c, const double* x0, const double* xr, const double* ur,
                       int64_t B, int N, int max_iters, double tol, double beta, double cc, double gamma0, int max_ls,
                       double* x, double* u, double* K1, double* sig, int32_t* n_iter, int32_t* status, double* cost,
                       int32_t* n_roll) {
-    const int64_t T = N - 1;
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t l = 0; l < B; l++)
-        solve_lane(m, c, x0 + 4 * l, xr, ur, N, max_iters, tol, beta, cc, gamma0, max_ls, x + 4 * N * l,
-                   u + 2 * T * l, K1 + 4 * T * l, sig + 2 * T * l, n_iter + l, status + l, cost + l, n_roll + l);
+    solve_batch(m, c, x0, xr, ur, B, N, max_iters, tol, beta, cc, gamma0, max_ls, x, u, K1, sig, n_iter, status, cost,
+                n_roll, NULL);
+}
+
+/* The same, with the per-iteration record of every lane: hist_* (B, hist_len), row-major per lane. */
+void orc_newton_solve_hist(const orc_model* m, const orc_cost* c, const double* x0, const double* xr,
+                           const double* ur, int64_t B, int N, int max_iters, double tol, double beta, double cc,
+                           double gamma0, int max_ls, double* x, double* u, double* K1, double* sig, int32_t* n_iter,
+                           int32_t* status, double* cost, int32_t* n_roll, int hist_len, double* hist_cost,
+                           double* hist_smax, int32_t* hist_trials, double* hist_margin) {
+    orc_hist h = {hist_len, hist_cost, hist_smax, hist_trials, hist_margin};
+    solve_batch(m, c, x0, xr, ur, B, N, max_iters, tol, beta, cc, gamma0, max_ls, x, u, K1, sig, n_iter, status, cost,
+                n_roll, &h);
 }
 
 /* Fixed number of Newton iterations per lane (no convergence stop) -- a bounded CPU sample for bench.py. */

@@ -46,6 +46,8 @@ def lib():
                                                     dp, dp, dp, dp, ip, ip, dp, ip]
         L.orc_newton_iters.argtypes = solve_args + [C.c_double, C.c_double, C.c_double, C.c_int,
                                                     dp, dp, dp, dp, ip, ip, dp, ip]
+        L.orc_newton_solve_hist.argtypes = solve_args + [C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
+                                                         dp, dp, dp, dp, ip, ip, dp, ip, C.c_int, dp, dp, ip, dp]
         L.orc_rk4.argtypes = [C.POINTER(Model), dp, dp, dp]
         L.orc_jac.argtypes = [C.POINTER(Model), dp, dp, dp, dp, dp]
         _lib = L
@@ -65,8 +67,13 @@ def cost(Q=(130.0, 30.0, 1e-4, 1e-4), R=(1e-6, 1.5), QT=(130.0, 130.0, 1.0, 1.0)
 
 
 def newton_solve(x0, x_ref, u_ref, max_iters=5000, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20,
-                 fixed_iters=None, params=PARAMS_1, weights=None):
-    """Batched solve on host cores (OpenMP). x0 (B,4). Returns dict like acrobot_np.newton_solve."""
+                 fixed_iters=None, params=PARAMS_1, weights=None, hist_len=0):
+    """Batched solve on host cores (OpenMP). x0 (B,4). Returns dict like acrobot_np.newton_solve.
+
+    hist_len > 0 adds the per-iteration record of every lane, (B, hist_len) arrays, NaN / 0 past a lane's last
+    iteration: ``hist_cost`` (cost after iteration k; unchanged on an LS failure), ``hist_smax`` (max|sigma| of its
+    sweep), ``hist_trials`` (Armijo trials evaluated) and ``hist_margin`` (the iteration's tightest Armijo test,
+    min |J_new - (J + c gamma dJ)| / |J| over its trials: how close the closest accept / reject call was to a tie)."""
     x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
     x_ref = np.ascontiguousarray(x_ref, np.float64)
     u_ref = np.ascontiguousarray(u_ref, np.float64)
@@ -79,7 +86,15 @@ def newton_solve(x0, x_ref, u_ref, max_iters=5000, tol=1e-4, beta=0.7, c=0.5, ga
                n_rollouts=np.zeros(B, np.int32))
     m = model(params); cw = cost(**(weights or {}))
     tail = (out["x"], out["u"], out["K1"], out["sigma"], out["n_iter"], out["status"], out["cost"], out["n_rollouts"])
-    if fixed_iters is None:
+    if hist_len and fixed_iters is None:
+        H = int(hist_len)
+        for k in ("hist_cost", "hist_smax", "hist_margin"):
+            out[k] = np.full((B, H), np.nan)
+        out["hist_trials"] = np.zeros((B, H), np.int32)
+        lib().orc_newton_solve_hist(C.byref(m), C.byref(cw), x0, x_ref, u_ref, B, N, max_iters, tol, beta, c,
+                                    gamma_0, max_ls, *tail, H, out["hist_cost"], out["hist_smax"],
+                                    out["hist_trials"], out["hist_margin"])
+    elif fixed_iters is None:
         lib().orc_newton_solve(C.byref(m), C.byref(cw), x0, x_ref, u_ref, B, N, max_iters, tol, beta, c, gamma_0,
                                max_ls, *tail)
     else:

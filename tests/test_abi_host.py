@@ -41,6 +41,10 @@ def test_library_build_id_matches_the_tree():
     assert len(want) == 16 and _build.embedded_build_id(path) == want
     assert _lib.load(path).gym_build_id().decode() == want
     assert not _build.needs_build()
+    # an A/B variant (extra defines) or another offload architecture carries another id, so it never passes for
+    # the canonical library
+    assert _build.source_hash(("GYM_TRACE=1",)) != want and _build.source_hash(arch="gfx942") != want
+    assert _build.source_hash(("B=1", "A=1")) == _build.source_hash(("A=1", "B=1"))
 
 
 def test_stale_library_is_refused(tmp_path):
@@ -156,6 +160,12 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
     need = C.c_int64()
     assert lib.gym_newton_tail_scratch(501, 3, 20, C.byref(need)) == 0 and need.value == 64 * (4 * 501 + 2 * 500)
     assert lib.gym_newton_tail_scratch(501, 3, 65, C.byref(need)) == 1                  # > 64 trials
+    # the tail's LDS at T = 500: above the 64 KiB default, within gfx950's 160 KiB (the device limit is queried
+    # only when asked for, so this runs without a device); horizons past the staging are refused
+    lds = C.c_int64()
+    assert lib.gym_newton_tail_lds(501, C.byref(lds), None) == 0 and 65536 < lds.value <= 160 * 1024
+    assert lib.gym_newton_tail_lds(641, C.byref(lds), None) == 0 and lds.value <= 160 * 1024
+    assert lib.gym_newton_tail_lds(642, C.byref(lds), None) == 1
     assert lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 3, D, need.value - 1, 0, 1, None) == 1   # scratch short
     assert lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 3, D, 1 << 40, 4, 2, None) == 1          # k1 < k0
     assert lib.gym_newton_iteration(R(m), R(w), R(_lib.GymArmijo(1e-4, 0.7, 0.5, 0.1, 0, 0)), R(b), 0, None) == 1
@@ -265,8 +275,28 @@ def test_symbolic_dynamics_surface_matches_reference(golden):
     ns = {}
     exec("from gymnast_optimalcontrol_amd.dynamics import *", ns)
     for n in ("theta1", "theta2", "M_func", "RHS_func", "f_cont_sym", "A_sym", "B_sym", "func_A", "func_B",
-              "M", "C", "Gvec", "F", "set_params", "dynamics", "dt", "params_1"):
+              "M", "C", "Gvec", "F", "set_params", "dynamics", "dt", "params_1",
+              "M11", "M12", "M21", "M22", "C11", "C12", "C21", "C22", "G1", "G2"):
         assert n in ns, n
+    # the module-level scalar entries (dynamics.py:64-83), as the reference writes them
+    S = {n: sp.Symbol(n) for n in ("I1", "I2", "l1", "lc1", "lc2", "m1", "m2", "g", "theta1", "theta2",
+                                   "theta1_dot", "theta2_dot")}
+    th1, th2, w1, w2 = S["theta1"], S["theta2"], S["theta1_dot"], S["theta2_dot"]
+    ref = {"M11": S["I1"] + S["I2"] + S["lc1"]**2 * S["m1"] + S["m2"] * (S["l1"]**2 + 2 * S["l1"] * S["lc2"] * sp.cos(th2)
+                                                                      + S["lc2"]**2),
+           "M12": S["I2"] + S["lc2"] * S["m2"] * (S["l1"] * sp.cos(th2) + S["lc2"]),
+           "M22": S["I2"] + S["lc2"]**2 * S["m2"],
+           "C11": -S["l1"] * S["lc2"] * S["m2"] * w2 * sp.sin(th2),
+           "C12": -S["l1"] * S["lc2"] * S["m2"] * (w1 + w2) * sp.sin(th2),
+           "C21": S["l1"] * S["lc2"] * S["m2"] * w1 * sp.sin(th2),
+           "G1": S["g"] * S["lc1"] * S["m1"] * sp.sin(th1) + S["g"] * S["m2"] * (S["l1"] * sp.sin(th1) + S["lc2"] *
+                                                                              sp.sin(th1 + th2)),
+           "G2": S["g"] * S["m2"] * S["lc2"] * sp.sin(th1 + th2)}
+    ref["M21"] = ref["M12"]
+    for n, e in ref.items():
+        assert sp.simplify(sp.expand(ns[n] - e)) == 0, n
+    assert ns["C22"] == 0
+    assert sp.simplify(ns["M"][0, 0] - ns["M11"]) == 0 and sp.simplify(ns["Gvec"][0] - ns["G1"]) == 0
     with pytest.raises(AttributeError):
         d.not_a_reference_name
 

@@ -75,7 +75,7 @@ def test_straggler_tail_is_bitwise_the_serial_schedule(kind):
         s = BatchedNewtonSolver(eng, xr, ur, B, **skw, **kw)
         assert s.tail_lanes > 0
         t = s.solve(x0, max_iters)
-        assert t.iterations == r.iterations or int(t.n_iter.max()) == int(r.n_iter.max()), name
+        assert t.iterations == r.iterations == int(r.n_iter.max()), name   # the last iteration a lane ran
         for f in FIELDS:
             _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{name}: {f}")
 
