@@ -128,17 +128,6 @@ template <int CP = kNT>
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, CP);
 }
-// GYM_MALL_STAGES (measurement variant, default 0 = off): the stages a pass writes last and the next pass reads
-// first (the sweep's lowest stages, the trial's highest knots) stored with the default cache policy instead of nt,
-// so that part of them might still be in the 256 MB Infinity Cache when the next pass starts reading there.  The
-// library-swapping A/B in one process favoured it slightly (profiles/r03/mall/ab_*.log), but bench.py in separate
-// processes on one box, alternating, measured 96 stages 1.7% SLOWER (bench_alternating_processes.log): off.
-#ifndef GYM_TRIAL_NEAR
-#define GYM_TRIAL_NEAR 1   // the solver trials' RK4 step on the near path without sub-step branches (gym::rk4_fast)
-#endif
-#ifndef GYM_MALL_STAGES
-#define GYM_MALL_STAGES 0
-#endif
 
 __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
 
@@ -155,24 +144,9 @@ template <int KIND>
 __device__ __forceinline__ void prio_start() {
     if (KIND != PRIO_NONE) __builtin_amdgcn_s_setprio(3);
 }
-// GYM_PRIO_SHIFT > 0 (measurement variant): cyclic bands of 2^shift stages, priority 3, 2, 1, 0, 3, ...
-#ifndef GYM_PRIO_SHIFT
-#define GYM_PRIO_SHIFT 0
-#endif
 template <int KIND>
 __device__ __forceinline__ void prio_band(int done, int T) {
     if (KIND == PRIO_NONE) return;
-    if (GYM_PRIO_SHIFT > 0) {
-        if ((done & ((1 << GYM_PRIO_SHIFT) - 1)) == 0) {
-            switch ((done >> GYM_PRIO_SHIFT) & 3) {
-                case 0: __builtin_amdgcn_s_setprio(3); break;
-                case 1: __builtin_amdgcn_s_setprio(2); break;
-                case 2: __builtin_amdgcn_s_setprio(1); break;
-                default: __builtin_amdgcn_s_setprio(0); break;
-            }
-        }
-        return;
-    }
     asm volatile("" : "+s"(T));   // thresholds recomputed per stage (3 SALU) rather than held: no spills
     if (done >= ((3 * T) >> 2)) __builtin_amdgcn_s_setprio(0);
     else if (done >= (T >> 1)) __builtin_amdgcn_s_setprio(1);
@@ -356,30 +330,16 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
         const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = v1 - urt[1];
         const KArgs ka = kernarg_consts();   // cost weights re-read per stage (no SGPR spills)
         J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xr + 4 * t, f0, f1);
-        const bool keep = GYM_MALL_STAGES > 0 && t >= T - GYM_MALL_STAGES;
         if (WRITE) {
             const auto rO = rsrc(Ob + (int64_t)t * row);
-            if (keep) {
-                if (!U0Z) bst1<0>(rO, o1, 0, v0);
-                bst1<0>(rO, o1, plane, v1);
-            } else {
-                if (!U0Z) bst1(rO, o1, 0, v0);             // U0Z: the u0 planes stay zero
-                bst1(rO, o1, plane, v1);
-            }
+            if (!U0Z) bst1(rO, o1, 0, v0);             // U0Z: the u0 planes stay zero
+            bst1(rO, o1, plane, v1);
         }
-        if (GYM_TRIAL_NEAR)
-            gym::rk4_fast(m, n0, n1, n2, n3, v1, pk);
-        else
-            gym::rk4(m, n0, n1, n2, n3, v1, pk);
+        gym::rk4_fast(m, n0, n1, n2, n3, v1, pk);      // near path without sub-step branches
         if (WRITE && (!CK || (t + 1) % CKI == 0 || t + 1 == T)) {   // CK: checkpoint knots only
             const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
-            if (keep) {
-                bst2<0>(rX, o2, 0, n0, n1);
-                bst2<0>(rX, o2, WROW, n2, n3);
-            } else {
-                bst2(rX, o2, 0, n0, n1);
-                bst2(rX, o2, WROW, n2, n3);
-            }
+            bst2(rX, o2, 0, n0, n1);
+            bst2(rX, o2, WROW, n2, n3);
         }
     };
     TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
@@ -554,120 +514,6 @@ struct Sweep {
     }
 };
 
-// ------------------------------------------------------------------------------------------
-// The Riccati update of Sweep::step_lin on a lane QUAD (lanes 4q .. 4q+3 of a wavefront hold one trajectory).
-// Lane r of the quad owns row r of P (all four entries: the symmetric matrix stored by rows) and p_r.  Per stage:
-//   Pb_r (own row)  ->  Pb and p broadcast in the quad (DPP)  ->  G11, g1, F_r, k_r, sigma1 (every lane the same
-//   uniform values; F_r in lane r)  ->  W row r = (P A_d)_r  ->  k, G11 k and the W rows exchanged through LDS
-//   ->  lane r evaluates row r of the new P: entry (r, j) is nP(min(r, j), max(r, j)), the upper-triangle entry
-//   the single-lane step computes, with the same expression (form and operands gathered per lane from LDS), so
-//   both copies of an off-diagonal entry are its bits  ->  p_r.
-// Every quantity is the single-lane step's expression with the same operands, compiled with FMA contraction
-// inside expressions only: the same bits (the schedules' bitwise tests run it against the single-lane sweep).
-// Where rows 0-1 and rows 2-3 use different forms (A_d rows 0, 1 are e1^T + dt e3^T, e2^T + dt e4^T), both forms
-// are evaluated and the lane's one selected.  About 80 fp64 instructions per lane and stage instead of ~200.
-// ------------------------------------------------------------------------------------------
-constexpr int QX_DOUBLES = 24;   // LDS exchange area per quad: W rows (16), (k_r, G11 k_r) pairs (8)
-template <int CTRL>
-__device__ __forceinline__ double qperm(double v) { return gym::dpp_d<CTRL>(v); }
-template <bool U0Z>
-struct QuadSweep {
-    double R0, R1, R2, R3, pr;   // row r of P, p_r
-    double dJ = 0.0, smax = 0.0;
-    int r;                       // this lane's row (lane & 3)
-    bool hi;                     // r >= 2
-    // per-lane LDS gather offsets of the row-r entries (slot j): W base row / col, A coefficient row i = min(r, j)
-    int ob[4], o2[4], o3[4], oi[4], ok[4];
-    double add[4];               // twoQ_r on the diagonal slot, -0.0 elsewhere (x + -0.0 == x, bit for bit)
-
-    __device__ __forceinline__ QuadSweep(const KW& w, int lane, double2 xa, double2 xb, const double* xrT) {
-        r = lane & 3;
-        hi = r >= 2;
-        const double qt = 2.0 * (r == 0 ? w.QT[0] : r == 1 ? w.QT[1] : r == 2 ? w.QT[2] : w.QT[3]);
-        R0 = r == 0 ? qt : 0.0; R1 = r == 1 ? qt : 0.0; R2 = r == 2 ? qt : 0.0; R3 = r == 3 ? qt : 0.0;
-        const double xv = r == 0 ? xa.x : r == 1 ? xa.y : r == 2 ? xb.x : xb.y;
-        const double xrv = r == 0 ? xrT[0] : r == 1 ? xrT[1] : r == 2 ? xrT[2] : xrT[3];
-        pr = qt * (xv - xrv);    // p_i = P_ii (x_i - xr_i), as the single-lane terminal condition
-        const double tq = r == 0 ? w.twoQ[0] : r == 1 ? w.twoQ[1] : r == 2 ? w.twoQ[2] : w.twoQ[3];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = r < j ? r : j, jj = r < j ? j : r;
-            ob[j] = (i >= 2 ? i - 2 : i) * 4 + jj;
-            o2[j] = 8 + jj;
-            o3[j] = 12 + jj;
-            oi[j] = i;
-            ok[j] = jj;
-            add[j] = (r == j) ? tq : -0.0;
-        }
-    }
-
-    // L: the stage's linearisation in LDS (stage_lin's fields in Lin order: A20..A23, A30..A33, bd2, bd3,
-    // q0..q3, r0, r1); X: this quad's exchange area.  Outputs the gain row k0..k3 and sigma (s0, s1) -- uniform.
-    __device__ __forceinline__ void step(double twoR1, double iG00, const double* L, double dt, double* X, double& k0,
-                                         double& k1, double& k2, double& k3, double& s0, double& s1) {
-#pragma clang fp contract(on)
-        const double bd2 = L[8], bd3 = L[9], r1 = L[15];
-        const double A2r = L[r], A3r = L[4 + r], qr = L[10 + r];
-        const double A20 = L[0], A21 = L[1], A22 = L[2], A23 = L[3];
-        const double A30 = L[4], A31 = L[5], A32 = L[6], A33 = L[7];
-        // Pb = P B_d[:,1]: row r here, then the rows the gain needs from the other lanes of the quad
-        const double Pbr = R2 * bd2 + R3 * bd3;
-        const double Pb2 = qperm<0xAA>(Pbr), Pb3 = qperm<0xFF>(Pbr), Pbh = qperm<0x44>(Pbr);
-        const double p2 = qperm<0xAA>(pr), p3 = qperm<0xFF>(pr), ph = qperm<0x44>(pr);
-        const double G11 = twoR1 + (bd2 * Pb2 + bd3 * Pb3);
-        // F row 1 = (P b)^T A_d, entry r (rows 0, 1 of A_d: [1 0 dt 0], [0 1 0 dt])
-        const double Fa = Pbh + A2r * Pb2 + A3r * Pb3;
-        const double Fb = dt * Pbh + A2r * Pb2 + A3r * Pb3;
-        const double F = hi ? Fb : Fa;
-        const double g1 = r1 + (bd2 * p2 + bd3 * p3);
-        const double iG = gym::recip(G11);
-        const double kr = -F * iG;
-        s1 = -g1 * iG;
-        if (U0Z) {
-            s0 = -0.0;
-            const double d1 = g1 * s1;
-            dJ += d1;
-        } else {
-            const double r0 = L[14];
-            s0 = -r0 * iG00;
-            dJ += r0 * s0 + g1 * s1;
-        }
-        const double gkr = G11 * kr;
-        // W row r = (P A_d)_r
-        const double W0 = R0 + R2 * A20 + R3 * A30, W1 = R1 + R2 * A21 + R3 * A31;
-        const double W2 = dt * R0 + R2 * A22 + R3 * A32, W3 = dt * R1 + R2 * A23 + R3 * A33;
-        X[16 + 2 * r] = kr; X[17 + 2 * r] = gkr;
-        X[4 * r + 0] = W0; X[4 * r + 1] = W1; X[4 * r + 2] = W2; X[4 * r + 3] = W3;
-        __builtin_amdgcn_wave_barrier();
-        // row r of P <- 2Q + A_d^T W - K^T G K, entry (r, j) = the upper-triangle entry (min, max)
-        double e[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const double Wb = X[ob[j]], Wt2 = X[o2[j]], Wt3 = X[o3[j]];
-            const double A2 = L[oi[j]], A3 = L[4 + oi[j]];
-            const double gk = X[17 + 2 * oi[j]], kj = X[16 + 2 * ok[j]];
-            double Y;
-            if (j < 2) {   // min(r, j) < 2: every lane uses the rows-0/1 form
-                Y = (Wb + A2 * Wt2 + A3 * Wt3) + add[j];
-            } else {
-                const double Ya = Wb + A2 * Wt2 + A3 * Wt3;
-                const double Yb = dt * Wb + A2 * Wt2 + A3 * Wt3;
-                Y = (hi ? Yb : Ya) + add[j];
-            }
-            e[j] = Y - gk * kj;
-        }
-        // p_r <- q_r + (A_d^T p)_r - k_r G11 sigma1
-        const double gs = G11 * s1;
-        const double npa = qr + (pr + A2r * p2 + A3r * p3) - kr * gs;
-        const double npb = qr + (dt * ph + A2r * p2 + A3r * p3) - kr * gs;
-        k0 = X[16]; k1 = X[18]; k2 = X[20]; k3 = X[22];
-        __builtin_amdgcn_wave_barrier();
-        R0 = e[0]; R1 = e[1]; R2 = e[2]; R3 = e[3];
-        pr = hi ? npb : npa;
-        smax = U0Z ? gym::nanmax_abs(smax, s1) : gym::nanmax_abs(gym::nanmax_abs(smax, s0), s1);
-    }
-};
-
 // API form: writes K row 1 (pairs), sigma planes and optionally lambda; register prefetch of stage t-1.
 template <bool LAMBDA>
 __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const double2* __restrict__ x,
@@ -726,15 +572,9 @@ __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int 
     const auto rC = rsrc(Cb + (int64_t)t * row);
     if (OUT != OUT_SIGMA) {
         const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        if (GYM_MALL_STAGES > 0 && t < GYM_MALL_STAGES) {
-            bst2<0>(rK, o2, 0, k0, k1);
-            bst2<0>(rK, o2, WROW, k2, k3);
-            bst1<0>(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
-        } else {
-            bst2(rK, o2, 0, k0, k1);
-            bst2(rK, o2, WROW, k2, k3);
-            bst1(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
-        }
+        bst2(rK, o2, 0, k0, k1);
+        bst2(rK, o2, WROW, k2, k3);
+        bst1(rC, o1, 0, stage_cg(xa, xb, ut1, g0, k0, k1, k2, k3, s1));
     }
     if (OUT != OUT_SOLVER) bst1(rC, o1, plane, s1);
 }
@@ -1688,23 +1528,12 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
 // (sweep -> trial) and x / u (trial -> next sweep), ordered by a fence per pass.  The waves of a SIMD drift
 // apart and mix sweep (HBM-heavy) and trial (fp64-heavy) passes by themselves, with no launch boundary, tail
 // or host round trip per iteration.  Per lane the arithmetic is the other schedules' (same device functions):
-// bit-identical results.
-// GYM_RUN_BAND (wave priority): 0 = none (default); 1 = the phase kernels' per-pass progress bands; 2 = cyclic
-// bands of the lane's iteration count.  Same-box A/B (B = 4096 / 32768 / 65536 lanes): 0 and 2 tie, 1 is 4-8%
-// slower (each pass restarting at priority 3 undoes the banding).
+// bit-identical results.  No wave priority bands (measured: the phase kernels' per-pass bands 4-8% slower here,
+// each pass restarting at priority 3 undoes them; cyclic bands of the iteration count no faster than none).
+// The kernel serves batches of at most 128 lanes per CU, i.e. at most one wavefront per SIMD, so it is compiled for
+// one (__launch_bounds__(BLK, 1)), and its sweep interleaves stage t-1's Jacobian with stage t's Riccati update
+// (backward_solver_lane_ilp).
 // ------------------------------------------------------------------------------------------
-#ifndef GYM_RUN_BAND
-#define GYM_RUN_BAND 0
-#endif
-// waves per SIMD the persistent kernel is compiled for: it serves batches of at most 96 lanes per CU, i.e. at
-// most one wavefront per SIMD, so its register budget need not leave room for more
-#ifndef GYM_RUN_WAVES
-#define GYM_RUN_WAVES 1
-#endif
-// the persistent kernel's sweep interleaves stage t-1's Jacobian with stage t's Riccati (backward_solver_lane_ilp)
-#ifndef GYM_RUN_ILP
-#define GYM_RUN_ILP 1
-#endif
 // Everything the kernel needs beyond the stage loops' own operands is one by-value struct whose fields are
 // re-read from the kernel-argument segment at each use (run_args(): scalar loads behind an opaque pointer),
 // so that none of its ~20 pointers is held in SGPRs across the stage loops (spilled, they cost v_readlane
@@ -1760,8 +1589,8 @@ __device__ unsigned long long g_run2_trace[8192][2][6];
 #define R2T_NOW() 0ull
 #endif
 template <bool U0Z, bool RL>
-__global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
-    constexpr bool BAND = GYM_RUN_BAND == 1;
+__global__ __launch_bounds__(BLK, 1) void k_nt_run(RunArgs args) {
+    constexpr bool BAND = false;
     const int64_t l = (int64_t)blockIdx.x * BLK + threadIdx.x;
     if (l >= args.B) return;
     // Nothing but the lane index, the iteration counter and the lane's status stays live across a pass: J, dJ,
@@ -1771,26 +1600,13 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
     for (int k = run_args()->k0; st == GYM_ACTIVE && k < run_args()->k1; ++k) {
         unsigned long long tt = R2T_NOW();
         ++acc[3];
-        if (GYM_RUN_BAND == 2) {
-            switch ((k >> 1) & 3) {
-                case 0: __builtin_amdgcn_s_setprio(3); break;
-                case 1: __builtin_amdgcn_s_setprio(2); break;
-                case 2: __builtin_amdgcn_s_setprio(1); break;
-                default: __builtin_amdgcn_s_setprio(0); break;
-            }
-        }
         const int cb = k & 1;
         {
             const rargs_t R = run_args();
             double d, s;
-            if (GYM_RUN_ILP)
-                backward_solver_lane_ilp<U0Z, OUT_SOLVER>(R->m, R->w, R->x[cb], R->u[cb], run_xr<RL>(R, l),
-                                                          run_ur<RL>(R, l), R->K1,
-                                                          R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
-            else
-                backward_solver_lane<U0Z, OUT_SOLVER, BAND>(R->m, R->w, R->x[cb], R->u[cb], run_xr<RL>(R, l),
-                                                            run_ur<RL>(R, l), R->K1,
-                                                            R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
+            backward_solver_lane_ilp<U0Z, OUT_SOLVER>(R->m, R->w, R->x[cb], R->u[cb], run_xr<RL>(R, l),
+                                                      run_ur<RL>(R, l), R->K1,
+                                                      R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
             const rargs_t Q = run_args();
             Q->dJ[l] = d;
             Q->smax[l] = s;
@@ -1877,43 +1693,20 @@ __global__ __launch_bounds__(BLK, GYM_RUN_WAVES) void k_nt_run(RunArgs args) {
 // Lanes that are not active (finished, padding) run along without storing anything: every barrier is reached by
 // every thread, and the iteration loop ends when no lane of the workgroup is active.
 // ------------------------------------------------------------------------------------------
-#ifndef GYM_RUN2_C
-#define GYM_RUN2_C 2
-#endif
-#ifndef GYM_RUN2_HELPERS
-#define GYM_RUN2_HELPERS 2
-#endif
-constexpr int R2C = GYM_RUN2_C;   // stages per chunk (even)
+constexpr int R2C = 2;            // stages per chunk (even)
 constexpr int R2S = 3 * R2C;      // ring slots (the trial uses two chunks of them, the split sweep three)
 constexpr int R2W = 11;           // pairs per lane and slot: sweep x_t (2), u_t, Lin (8); trial x_{t+1} (2), u1_t
-#ifndef GYM_RUN2_PAIR
-#define GYM_RUN2_PAIR 1
-#endif
-#ifndef GYM_RUN2_SPLIT
-#define GYM_RUN2_SPLIT 1
-#endif
-// GYM_RUN2_SPLIT (with the lane-pair wavefront, GYM_RUN2_PAIR): the sweep's Riccati update is split over two
-// wavefronts, the main one running only the matrix half (Sweep::step_P: gain row, P) and handing k, G11, 1/G11 to
-// the pair wavefront, which runs the vector half (step_p: sigma, dJ, p, ||sigma||) and the K1 / cg stores one chunk
-// behind.  Nothing flows back, so the main wavefront's chain loses the vector half, the stores and 6 of its 11
-// ring reads per stage.  The helpers' ring is then three chunks deep (the pair wavefront reads chunk c - 1 while
-// the main one reads c and the helpers write c + 1).
-constexpr bool R2SPLIT = GYM_RUN2_SPLIT && GYM_RUN2_PAIR;
-constexpr int R2RD = R2SPLIT ? 3 : 2;   // helper ring depth in chunks (sweep)
-#ifndef GYM_RUN2_PD
-#define GYM_RUN2_PD 4
-#endif
+// The sweep's Riccati update is split over two wavefronts: the main one runs only the matrix half (Sweep::step_P:
+// gain row, P) and hands k, G11, 1/G11 to the pair wavefront, which runs the vector half (step_p: sigma, dJ, p,
+// ||sigma||) and the K1 / cg stores one chunk behind.  Nothing flows back, so the main wavefront's chain loses the
+// vector half, the stores and 6 of its 11 ring reads per stage.  The helpers' ring is three chunks deep (the pair
+// wavefront reads chunk c - 1 while the main one reads c and the helpers write c + 1).
+constexpr int R2RD = 3;           // helper ring depth in chunks (sweep)
 // Prefetch distance of the producers' stream loads, in stages (= register sets in rotation).  A stage of either
-// wavefront is now ~2x shorter than the single-wavefront kernel's, and the loads of data the previous pass wrote
+// wavefront is ~2x shorter than the single-wavefront kernel's, and the loads of data the previous pass wrote
 // take ~1 us: with one stage of prefetch both passes ran at the load latency (~2,400 cycles per stage measured,
 // whatever the instruction count, tools/run2_trace.py).
-constexpr int R2PD = GYM_RUN2_PD;
-#ifndef GYM_RUN2_SWEEP_VGPR
-#define GYM_RUN2_SWEEP_VGPR 1   // the sweep roles' constants held in VGPRs across their stage loops
-#endif
-#ifndef GYM_RUN2_DYN_SGPR
-#define GYM_RUN2_DYN_SGPR 0   // measurement variant: the trial's model coefficients held in SGPRs
-#endif
+constexpr int R2PD = 4;
 static_assert(R2PD % R2C == 0, "the prefetch distance is a whole number of chunks");
 // chunks per pass, rounded up to whole register-set rotations: producer and consumer both run this many chunk
 // phases (the consumer skips the stages past T), so their barrier counts match
@@ -1976,7 +1769,6 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
     const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
     // x_ref / u_ref rows: wave-uniform scalar loads (restrict parameters: no store can alias them); per-lane
     // references (RL): the lane's own rows
-#if GYM_RUN2_SWEEP_VGPR
     // the model, the weights stage_lin reads and every Horner coefficient held in VGPRs across the stage loop: no
     // per-stage kernel-argument loads (and their lgkmcnt(0) waits) and no per-use copies of scalar operands
     const gym::PolyRegs pk = gym::poly_vgprs_all();
@@ -1987,9 +1779,6 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
     gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
     gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
     gym::in_vgpr(wv.G00); gym::in_vgpr(wv.twoR1);
-#else
-    const gym::PolyRegs pk = gym::poly_vgprs();
-#endif
     auto fetch = [&](SweepStage& q, int t) {
         const auto rX = rsrc(Xb + (int64_t)t * (2 * (int64_t)row)), rU = rsrc(Ub + (int64_t)t * row);
         q.xa = bld2(rX, o2, 0);
@@ -1998,18 +1787,10 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
         q.u1 = bld1(rU, o1, plane);
     };
     auto produce = [&](const SweepStage& q, int t, int slot) {
-#if GYM_RUN2_SWEEP_VGPR
         const gym::Jac J = gym::jacobian(dm, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
         const Row<4> xrt = ref_row<4, RL>(xr, t);
         const Row<2> urt = ref_row<2, RL>(ur, t);
         const Lin L = stage_lin<U0Z>(dm, wv, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
-#else
-        const KArgs ka = kernarg_consts();
-        const gym::Jac J = gym::jacobian(ka.m, q.xa.x, q.xa.y, q.xb.x, q.xb.y, q.u1, pk);
-        const Row<4> xrt = ref_row<4, RL>(xr, t);
-        const Row<2> urt = ref_row<2, RL>(ur, t);
-        const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, q.xa, q.xb, q.u0, q.u1, xrt.v, urt.v);
-#endif
         double2(*s)[BLK] = ring[slot];
         s[0][lane] = q.xa;                          s[1][lane] = q.xb;
         s[2][lane] = make_double2(q.u0, q.u1);      s[3][lane] = make_double2(L.A20, L.A21);
@@ -2044,50 +1825,10 @@ __device__ __forceinline__ void run2_sweep_helper(ring_t ring, int lane, int64_t
         }
     }
     lds_barrier(bw);
-    if (R2SPLIT) lds_barrier(bw);          // the vector half's last chunk
+    lds_barrier(bw);                       // the vector half's last chunk
 }
 
-// main wavefront, sweep: the Riccati recursion from the ring; K row 1 / cg stored for active lanes
-template <bool U0Z, bool RL>
-__device__ __forceinline__ void run2_sweep_main(ring_t ring, int lane, int64_t l, int cb, bool act, double& dJ_out,
-                                                double& smax_out, unsigned long long& bw) {
-    const rargs_t R = run_args();
-    const int T = R->N - 1;
-    const int64_t Bp = R->Bp;
-    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
-    const char* Kb = reinterpret_cast<const char*>(R->K1);
-    const char* Cb = reinterpret_cast<const char*>(R->cs);
-    const double g0 = R->a.gamma0;
-    const double2* x = R->x[cb];
-    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], run_xr<RL>(R, l) + 4 * T);
-    const int nch = run2_chunks(T);
-    lds_barrier(bw);                       // the helper's chunk 0
-    for (int c = 0; c < nch; ++c) {
-#pragma unroll
-        for (int j = 0; j < R2C; ++j) {
-            const int i = c * R2C + j;
-            if (i < T) {
-                const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
-                const double2 xa = s[0][lane], xb = s[1][lane], uu = s[2][lane];
-                const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
-                const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
-                const KArgs ka = kernarg_consts();
-                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
-                            qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
-                double k0, k1, k2, k3, s0, s1;
-                S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
-                if (act) store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, k0, k1, k2,
-                                                 k3, s1);
-            }
-        }
-        lds_barrier(bw);
-    }
-    dJ_out = S.dJ;
-    smax_out = S.smax;
-}
-
-// GYM_RUN2_SPLIT, main wavefront, sweep: the matrix half of the Riccati recursion (Sweep::step_P) from the ring's
+// main wavefront, sweep: the matrix half of the Riccati recursion (Sweep::step_P) from the ring's
 // A_d rows and b; stage i's gain row, G11 and 1/G11 into the gain ring (slot (c & 1) * R2C + j) for the pair
 // wavefront.  Chunk c between barriers c and c + 1, as run2_sweep_main.
 typedef double2 (*gring_t)[3][BLK];
@@ -2099,12 +1840,10 @@ __device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int 
     const double2* x = R->x[cb];
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, R->Bp)], x[wix(T, 1, 2, l, R->Bp)], run_xr<RL>(R, l) + 4 * T);
     const int nch = run2_chunks(T);
-#if GYM_RUN2_SWEEP_VGPR
     KW wv = R->w;                          // step_P's weights and dt in VGPRs: no per-stage kernel-argument loads
     double dtv = R->m.h;
     gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
     gym::in_vgpr(wv.twoR1); gym::in_vgpr(dtv);
-#endif
     lds_barrier(bw);                       // the helpers' chunk 0
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
@@ -2114,18 +1853,10 @@ __device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int 
                 const double2(*s)[BLK] = ring[(c % R2RD) * R2C + j];
                 const double2 a0 = s[3][lane], a1 = s[4][lane], a2 = s[5][lane], a3 = s[6][lane];
                 const double2 bd = s[7][lane];
-#if GYM_RUN2_SWEEP_VGPR
                 const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
                             0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dtv};      // q, r: the vector half's
                 double k0, k1, k2, k3, G11, iG;
                 S.step_P(wv, L, k0, k1, k2, k3, G11, iG);
-#else
-                const KArgs ka = kernarg_consts();
-                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
-                            0.0, 0.0, 0.0, 0.0, 0.0, 0.0, ka.m.h};   // q, r: the vector half's
-                double k0, k1, k2, k3, G11, iG;
-                S.step_P(ka.w, L, k0, k1, k2, k3, G11, iG);
-#endif
                 double2(*g)[BLK] = gring[(c & 1) * R2C + j];
                 g[0][lane] = make_double2(k0, k1);
                 g[1][lane] = make_double2(k2, k3);
@@ -2137,7 +1868,7 @@ __device__ __forceinline__ void run2_sweep_gain(ring_t ring, gring_t gring, int 
     lds_barrier(bw);                       // the vector half's last chunk
 }
 
-// GYM_RUN2_SPLIT, pair wavefront, sweep: the vector half (Sweep::step_p) of stage i from the helpers' ring (chunk
+// pair wavefront, sweep: the vector half (Sweep::step_p) of stage i from the helpers' ring (chunk
 // c, still in its slot: three chunks deep) and the main wavefront's gain ring; K row 1 / cg stored for active lanes.
 // Chunk c between barriers c + 1 and c + 2.
 template <bool U0Z, bool RL>
@@ -2155,11 +1886,9 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
     const double2* x = R->x[cb];
     Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], run_xr<RL>(R, l) + 4 * T);
     const int nch = run2_chunks(T);
-#if GYM_RUN2_SWEEP_VGPR
     KW wv = R->w;                          // step_p's weights and dt in VGPRs: no per-stage kernel-argument loads
     double dtv = R->m.h;
     gym::in_vgpr(wv.iG00); gym::in_vgpr(dtv);
-#endif
     lds_barrier(bw);                       // the helpers' chunk 0
     lds_barrier(bw);                       // the main wavefront's chunk 0
     for (int c = 0; c < nch; ++c) {
@@ -2173,18 +1902,10 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
                 const double2 bd = s[7][lane], qa = s[8][lane], qb = s[9][lane], rr = s[10][lane];
                 const double2(*g)[BLK] = gring[(c & 1) * R2C + j];
                 const double2 ka01 = g[0][lane], ka23 = g[1][lane], gi = g[2][lane];
-#if GYM_RUN2_SWEEP_VGPR
                 const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
                             qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, dtv};
                 double s0, s1;
                 S.step_p<U0Z>(wv, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
-#else
-                const KArgs ka = kernarg_consts();
-                const Lin L{a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, bd.x, bd.y,
-                            qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, ka.m.h};
-                double s0, s1;
-                S.step_p<U0Z>(ka.w, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
-#endif
                 if (act) {
                     if (ext)   // external retries: sigma1 stored too (the candidates read it; no re-run)
                         store_stage<OUT_ALL>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
@@ -2201,155 +1922,17 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
     smax_out = S.smax;
 }
 
-// main wavefront, first Armijo trial: feedback + RK4 chain; (x_{t+1}, u1_t) into the ring
-template <bool U0Z>
-__device__ __forceinline__ void run2_trial_main(ring_t ring, int lane, int64_t l, int cb, unsigned long long& bw) {
-    const rargs_t R = run_args();
-    const int T = R->N - 1;
-    const int64_t Bp = R->Bp;
-    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u;
-    const char* Kb = reinterpret_cast<const char*>(R->K1);
-    const char* Cb = reinterpret_cast<const char*>(R->cs);
-    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
-    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
-    auto fetch = [&](TrialStage& q, int t) {
-        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        q.k0 = bld2(rK, o2, 0);
-        q.k1 = bld2(rK, o2, WROW);
-        q.cg = bld1(rsrc(Cb + (int64_t)t * row), o1, 0);
-    };
-    const gym::PolyRegs pk = gym::poly_vgprs();
-#if GYM_RUN2_DYN_SGPR
-    const Dyn dm = R->m;                   // held in SGPRs across the stage loop
-#endif
-    auto step = [&](const TrialStage& q, int slot) {
-        const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
-#if GYM_RUN2_DYN_SGPR
-        gym::rk4(dm, n0, n1, n2, n3, v1, pk);
-#else
-        const KArgs ka = kernarg_consts();
-        gym::rk4(ka.m, n0, n1, n2, n3, v1, pk);
-#endif
-        double2(*s)[BLK] = ring[slot];
-        s[0][lane] = make_double2(n0, n1);
-        s[1][lane] = make_double2(n2, n3);
-        s[2][lane] = make_double2(v1, 0.0);
-    };
-    const int nch = run2_chunks(T);        // branch-free stream loads (see run2_sweep_helper)
-    TrialStage P[R2PD];                    // stage t's streams in set t % R2PD, loaded R2PD stages ahead
-#pragma unroll
-    for (int j = 0; j < R2PD; ++j) fetch(P[j], uni(min(j, T - 1)));
-    for (int c0 = 0; c0 < nch; c0 += R2PD / R2C) {
-#pragma unroll
-        for (int cc = 0; cc < R2PD / R2C; ++cc) {
-            const int c = c0 + cc;
-#pragma unroll
-            for (int j = 0; j < R2C; ++j) {
-                const int t = c * R2C + j, set = cc * R2C + j;
-                step(P[set], (c & 1) * R2C + j);   // past the end: harmless, not consumed
-                fetch(P[set], uni(min(t + R2PD, T - 1)));
-            }
-            lds_barrier(bw);
-        }
-    }
-    lds_barrier(bw);
-}
-
-#ifndef GYM_RUN2_PAIR_VOP3
-#define GYM_RUN2_PAIR_VOP3 1   // three-address Horner steps in the pair trial (acrobot_device.hpp hfma)
-#endif
-#ifndef GYM_RUN2_TRIAL_COPY
-#define GYM_RUN2_TRIAL_COPY 1
-#endif
-#ifndef GYM_RUN2_FETCH0
-#define GYM_RUN2_FETCH0 0   // measurement variant (wrong results): every trial stage re-reads stage 0's K row / cg
-#endif
-// the first Armijo trial's chain on a lane pair (GYM_RUN2_PAIR): two wavefronts share the 64 lanes' RK4 chains,
-// trajectory tl (< 64) of the workgroup on lanes (2q, 2q+1) of wavefront tl / 32 with q = tl % 32; the even lane
-// reduces / rotates th1, the odd lane th2 (gym::rk4_pair, bit-identical to rk4); the ring receives the same rows
-template <bool U0Z>
-__device__ __forceinline__ void run2_trial_main_pair(ring_t ring, int tl, int64_t l, bool odd, int cb,
-                                                     unsigned long long& bw) {
-    const rargs_t R = run_args();
-    const int T = R->N - 1;
-    const int64_t Bp = R->Bp;
-    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u;
-    const char* Kb = reinterpret_cast<const char*>(R->K1);
-    const char* Cb = reinterpret_cast<const char*>(R->cs);
-    const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
-    double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
-    auto fetch = [&](TrialStage& q, int t) {
-        const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
-        q.k0 = bld2(rK, o2, 0);
-        q.k1 = bld2(rK, o2, WROW);
-        q.cg = bld1(rsrc(Cb + (int64_t)t * row), o1, 0);
-    };
-    const gym::PolyRegs pk = gym::poly_vgprs();
-    const int prow = odd ? 1 : 0;
-    auto step = [&](const TrialStage& q, int slot) {
-        const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
-        const KArgs ka = kernarg_consts();
-        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, v1, pk);
-        double2(*s)[BLK] = ring[slot];
-        s[prow][tl] = odd ? make_double2(n2, n3) : make_double2(n0, n1);
-        s[2][tl] = make_double2(v1, 0.0);   // both lanes of the pair: the same value
-    };
-    const int nch = run2_chunks(T);        // branch-free stream loads (see run2_sweep_helper)
-    TrialStage P[R2PD];
-#pragma unroll
-    for (int j = 0; j < R2PD; ++j) fetch(P[j], uni(min(j, T - 1)));
-    for (int c0 = 0; c0 < nch; c0 += R2PD / R2C) {
-#pragma unroll
-        for (int cc = 0; cc < R2PD / R2C; ++cc) {
-            const int c = c0 + cc;
-#pragma unroll
-            for (int j = 0; j < R2C; ++j) {
-                const int t = c * R2C + j, set = cc * R2C + j;
-                if (GYM_RUN2_TRIAL_COPY) {
-                    // the stage's streams moved out of the loading registers first (as run2_sweep_helper): the
-                    // wait is then for this set alone, R2PD stages old, and the set is re-armed at once
-                    TrialStage w = P[set];
-                    in_vgpr2(w.k0); in_vgpr2(w.k1); gym::in_vgpr(w.cg);
-                    fetch(P[set], GYM_RUN2_FETCH0 ? 0 : uni(min(t + R2PD, T - 1)));
-                    step(w, (c & 1) * R2C + j);
-                } else {
-                    step(P[set], (c & 1) * R2C + j);
-                    fetch(P[set], uni(min(t + R2PD, T - 1)));
-                }
-            }
-            lds_barrier(bw);
-        }
-    }
-    lds_barrier(bw);
-}
-
-#ifndef GYM_RUN2_KLOAD
-#define GYM_RUN2_KLOAD 1
-#endif
-#ifndef GYM_RUN2_KLOAD_SGPR
-#define GYM_RUN2_KLOAD_SGPR 1
-#endif
-#ifndef GYM_RUN2_DYN_VGPR
-#define GYM_RUN2_DYN_VGPR 1
-#endif
-#ifndef GYM_RUN2_POLY_ALL
-#define GYM_RUN2_POLY_ALL 1   // every Horner coefficient of the chain's minimax kernels held in VGPRs (gym::poly_vgprs_all)
-#endif
-#ifndef GYM_RUN2_NEAR
-#define GYM_RUN2_NEAR 1   // the chain's RK4 step branch-free on the near path (gym::rk4_pair_fast)
-#endif
-// GYM_RUN2_KLOAD (with the lane-pair trial and two sweep helpers): the second sweep helper, idle in the trial, becomes
-// the trial's loader.  It reads K row 1 and cg of the stages two chunks ahead from global memory and writes them into
+// The first Armijo trial's chain runs on lane pairs: two wavefronts share the 64 lanes' RK4 chains, trajectory
+// tl (< 64) of the workgroup on lanes (2q, 2q+1) of wavefront tl / 32 with q = tl % 32; the even lane reduces /
+// rotates th1, the odd lane th2 (gym::rk4_pair_fast, bit-identical to rk4).  The second sweep helper, idle in the
+// trial, is the chains' loader.  It reads K row 1 and cg of the stages two chunks ahead from global memory and writes them into
 // an LDS ring three chunks deep ([slot][k0, k1, cg][trajectory]); the two RK4-chain wavefronts read each stage's row
 // from LDS one stage ahead and issue no global loads at all.  With the global loads on the chains the compiler's
 // wait-count placement (loop rotation around the branchy RK4 step) waited for the most recent prefetches once per
 // unrolled body: a load round trip on the chain.  The loader waits for its own loads, off every chain.
-constexpr bool R2KLOAD = GYM_RUN2_KLOAD && R2SPLIT && GYM_RUN2_HELPERS == 2;
 typedef double2 (*kring_t)[3][BLK];
 
-// loader wavefront (GYM_RUN2_KLOAD): chunks 0, 1 before the pass's leading barrier, chunk c + 2 during phase c
+// loader wavefront: chunks 0, 1 before the pass's leading barrier, chunk c + 2 during phase c
 template <bool U0Z>
 __device__ __forceinline__ void run2_trial_kload(kring_t kr, int lane, int64_t l, unsigned long long& bw) {
     const rargs_t R = run_args();
@@ -2395,7 +1978,7 @@ __device__ __forceinline__ void run2_trial_kload(kring_t kr, int lane, int64_t l
     lds_barrier(bw);
 }
 
-// the pair trial's chain (run2_trial_main_pair) fed from the loader's LDS ring: stage t's row is read during stage
+// the pair trial's chain fed from the loader's LDS ring: stage t's row is read during stage
 // t - 1 (chunk c + 1's first row during chunk c's last stage: written in phase c - 1)
 template <bool U0Z>
 __device__ __forceinline__ void run2_trial_pair_lds(ring_t ring, kring_t kr, int tl, int64_t l, bool odd, int cb,
@@ -2410,29 +1993,18 @@ __device__ __forceinline__ void run2_trial_pair_lds(ring_t ring, kring_t kr, int
         q.k1 = kr[slot][1][tl];
         q.cg = kr[slot][2][tl].x;
     };
-    const gym::PolyRegs pk = GYM_RUN2_POLY_ALL ? gym::poly_vgprs_all() : gym::poly_vgprs();
-#if GYM_RUN2_KLOAD_SGPR
-    // the model held in registers across the stage loop: no scalar loads in it, so the LDS reads' lgkmcnt waits are
-    // not merged with kernarg loads (GYM_RUN2_DYN_VGPR: in VGPRs, so that no instruction needs a per-stage copy of a
-    // second scalar operand)
+    // every Horner coefficient of the minimax kernels and the model held in VGPRs across the stage loop: no scalar
+    // loads in it (the LDS reads' lgkmcnt waits are not merged with kernarg loads) and no per-stage copies of second
+    // scalar operands
+    const gym::PolyRegs pk = gym::poly_vgprs_all();
     Dyn dm = R->m;
-    if (GYM_RUN2_DYN_VGPR) {
-        gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
-        gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
-        gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
-    }
-#endif
+    gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+    gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+    gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
     auto step = [&](const TrialStage& q, int slot) {
         const double v1 = trial_u1(q.k0, q.k1, q.cg, n0, n1, n2, n3);
-#if GYM_RUN2_KLOAD_SGPR
-        if (GYM_RUN2_NEAR)
-            gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
-        else
-            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(dm, odd, n0, n1, n2, n3, v1, pk);
-#else
-        const KArgs ka = kernarg_consts();
-        gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(ka.m, odd, n0, n1, n2, n3, v1, pk);
-#endif
+        // branch-free near-path step (a wave-uniform fallback to the full reduction inside); three-address Horner
+        gym::rk4_pair_fast<true>(dm, odd, n0, n1, n2, n3, v1, pk);
         double2(*s)[BLK] = ring[slot];
         s[0][tl] = make_double2(n0, n1);    // both lanes of the pair: the same values, no per-lane select
         s[1][tl] = make_double2(n2, n3);
@@ -2483,7 +2055,7 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     }
     double J = 0.0;
     const int nch = run2_chunks(T);
-    if (R2KLOAD) lds_barrier(bw);          // the loader's leading barrier
+    lds_barrier(bw);                       // the loader's leading barrier
     lds_barrier(bw);                       // the main wavefront's chunk 0
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
@@ -2517,24 +2089,17 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     return J + xcost(R->w.QT, n0, n1, n2, n3, xrT.v);
 }
 
-constexpr int R2H = GYM_RUN2_HELPERS;   // helper wavefronts: the sweep's stages are dealt to them round-robin
-static_assert(R2H == 1 || R2H == 2, "one or two helper wavefronts");
-// GYM_RUN2_PAIR: a further wavefront (index R2H + 1) joins the main one in the trial, each trajectory's RK4 chain
-// on a lane pair (run2_trial_main_pair); it idles through the sweep
-constexpr int R2P = GYM_RUN2_PAIR;
-constexpr int R2WAVES = 1 + R2H + R2P;
-
-// a helper wavefront that has no part in a pass still takes part in its chunk barriers
-__device__ __forceinline__ void run2_idle(int T, unsigned long long& bw) {
-    const int nch = run2_chunks(T);
-    for (int c = 0; c <= nch; ++c) lds_barrier(bw);
-}
+// Four wavefronts per 64 lanes.  Sweep: 0 the matrix half of the Riccati update, 1 and 2 the stage linearisations
+// (dealt round-robin), 3 the vector half and the stores.  Trial: 0 and 3 the RK4 chains on lane pairs, 1 the cost
+// and the candidate's stores, 2 the chains' loader.
+constexpr int R2H = 2;            // sweep helper wavefronts
+constexpr int R2WAVES = 4;
 
 template <bool U0Z, bool RL>
 __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
     __shared__ double2 ring[R2S][R2W][BLK];
-    __shared__ double2 gring[R2SPLIT ? 2 * R2C : 1][3][BLK];   // GYM_RUN2_SPLIT: gain rows, G11, 1/G11
-    __shared__ double2 kring[R2KLOAD ? 3 * R2C : 1][3][BLK];   // GYM_RUN2_KLOAD: the trial's K row 1 / cg
+    __shared__ double2 gring[2 * R2C][3][BLK];   // the split sweep's gain rows, G11, 1/G11
+    __shared__ double2 kring[3 * R2C][3][BLK];   // the trial's K row 1 / cg (loader wavefront)
     __shared__ double shJ[BLK];
     __shared__ int shst[BLK];
     const int lane = threadIdx.x & (BLK - 1);
@@ -2553,19 +2118,14 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
         if (wave == 1) {
             run2_sweep_helper<U0Z, 0, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l), run_ur<RL>(run_args(), l),
                                                acc[4]);
-        } else if (wave == 2 && R2H == 2) {
-            run2_sweep_helper<U0Z, R2H - 1, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l),
-                                                     run_ur<RL>(run_args(), l), acc[4]);
-        } else if (wave > R2H && !R2SPLIT) {
-            run2_idle(run_args()->N - 1, acc[4]);
-        } else if (wave == 0 && R2SPLIT) {
+        } else if (wave == 2) {
+            run2_sweep_helper<U0Z, 1, R2H, RL>(ring, lane, l, cb, run_xr<RL>(run_args(), l),
+                                               run_ur<RL>(run_args(), l), acc[4]);
+        } else if (wave == 0) {
             run2_sweep_gain<U0Z, RL>(ring, gring, lane, l, cb, acc[4]);
-        } else {   // the main wavefront, or with GYM_RUN2_SPLIT the pair wavefront (the vector half, the stores)
+        } else {   // the pair wavefront: the vector half, the stores
             double d, s;
-            if (R2SPLIT)
-                run2_sweep_vec<U0Z, RL>(ring, gring, lane, l, cb, act, d, s, acc[4]);
-            else
-                run2_sweep_main<U0Z, RL>(ring, lane, l, cb, act, d, s, acc[4]);
+            run2_sweep_vec<U0Z, RL>(ring, gring, lane, l, cb, act, d, s, acc[4]);
             const rargs_t Q = run_args();
             if (act) {
                 Q->dJ[l] = d;
@@ -2574,24 +2134,17 @@ __global__ __launch_bounds__(R2WAVES * BLK, 1) void k_nt_run2(RunArgs args) {
             }
             lane_fence();                                  // K1 / cg visible to this wavefront's trial loads
         }
-        if (R2P) __syncthreads();                          // K1 / cg stored by the main wavefront, read by both
+        __syncthreads();                                   // K1 / cg stored by the pair wavefront, read by the loader
         acc[0] += R2T_NOW() - tt;
         tt = R2T_NOW();
         if (wave == 1) {
             shJ[lane] = run2_trial_helper<U0Z, RL>(ring, lane, l, cb, act, run_xr<RL>(run_args(), l),
                                                    run_ur<RL>(run_args(), l), acc[5]);
-        } else if (wave == 2 && R2KLOAD) {
+        } else if (wave == 2) {
             run2_trial_kload<U0Z>(kring, lane, l, acc[5]);
-        } else if (wave == 2 && R2H == 2) {
-            run2_idle(run_args()->N - 1, acc[5]);
-        } else if (R2P && R2KLOAD) {                       // wave 0 and wave R2H + 1: lane pairs, rows from LDS
+        } else {                                           // waves 0 and 3: lane pairs, rows from LDS
             const int tl = (wave == 0 ? 0 : BLK / 2) + (lane >> 1);
             run2_trial_pair_lds<U0Z>(ring, kring, tl, (int64_t)blockIdx.x * BLK + tl, lane & 1, cb, acc[5]);
-        } else if (R2P) {                                  // wave 0 and wave R2H + 1: lane pairs
-            const int tl = (wave == 0 ? 0 : BLK / 2) + (lane >> 1);
-            run2_trial_main_pair<U0Z>(ring, tl, (int64_t)blockIdx.x * BLK + tl, lane & 1, cb, acc[5]);
-        } else {
-            run2_trial_main<U0Z>(ring, lane, l, cb, acc[5]);
         }
         __syncthreads();                                   // shJ written; the helper's stores are complete
         acc[1] += R2T_NOW() - tt;
@@ -2707,118 +2260,29 @@ __device__ __forceinline__ targs_t tail_args() {
     return (targs_t)p;
 }
 
-// GYM_TAIL_QUAD (measurement variant): the tail sweep's Riccati recursion on lane quads (QuadSweep; every quad of
-// the wavefront runs the lane's recursion, the same bits) instead of on every thread (Sweep::step_lin).  Measured
-// slower (latency-bound exchanges), so off by default.
-#ifndef GYM_TAIL_QUAD
-#define GYM_TAIL_QUAD 0
-#endif
 // The trials' per-stage inputs are staged in LDS by the sweep (K row 1, cg, sigma1 and u0: 8 doubles per stage), so
 // the trial loop issues no global loads: its scratch stores are never waited on (the GFX9 vmcnt counts both)
 constexpr int TL_TST = 8;
 constexpr int TL_MAX_T = 640;    // T * 64 B of trial staging (40 KiB) + the linearisation / gain / exchange areas: tail_lds_bytes(T),
                                  // ~72 KiB at T = 500, ~87 KiB at T = 640: above the 64 KiB default, so every launch raises
                                  // the kernel's dynamic-LDS limit (gfx950: 160 KiB); gym_newton_tail_lds reports both
-#ifndef GYM_TAIL_SPLIT
-#define GYM_TAIL_SPLIT 1
-#endif
-#ifndef GYM_TAIL_SWEEP_VGPR
-#define GYM_TAIL_SWEEP_VGPR 1   // the split tail sweep's weights held in VGPRs across its stage loops
-#endif
-#ifndef GYM_TAIL_CHAIN_VGPR
-#define GYM_TAIL_CHAIN_VGPR 1
-#endif
-#ifndef GYM_TAIL_NEAR
-#define GYM_TAIL_NEAR 1   // the trials' RK4 chains branch-free on the near path (gym::rk4_pair_fast, as k_nt_run2)
-#endif
-// GYM_TAIL_SPLIT: two wavefronts per tail lane, the sweep's Riccati update split as in k_nt_run2 (Sweep::step_P on
-// wavefront 0, Sweep::step_p, the stores and the next pass's linearisations on wavefront 1, one 64-stage pass
-// behind; linearisations triple-buffered, the gain rows double-buffered); the trials stay on wavefront 0
-constexpr bool TL_SPLIT = GYM_TAIL_SPLIT && !GYM_TAIL_QUAD;
-constexpr int TL_THREADS = TL_SPLIT ? 2 * BLK : BLK;
+// Two wavefronts per tail lane: the sweep's Riccati update split as in k_nt_run2 (Sweep::step_P on wavefront 0,
+// Sweep::step_p, the stores and the next pass's linearisations on wavefront 1, one 64-stage pass behind;
+// linearisations triple-buffered, the gain rows double-buffered)
+constexpr int TL_THREADS = 2 * BLK;
 constexpr int TL_GK = 6;         // doubles per stage in the gain ring: k row 1 (4), G11, 1/G11
-// TL_SPLIT trials: wavefront 0 runs the candidates' RK4 chains on lane pairs and hands each stage's (x_{t+1}, u1_t)
-// to wavefront 1 through a ring of 2 chunks x TL_RC stages x 32 trials x 3 pairs; wavefront 1 (lane c: trial c)
-// accumulates the cost and stores the candidate
+// Trials on lane pairs: wavefront 0 runs the candidates' RK4 chains and hands each stage's (x_{t+1}, u1_t) to
+// wavefront 1 through a ring of 2 chunks x TL_RC stages x 32 trials x 3 pairs; wavefront 1 (lane c: trial c)
+// accumulates the cost and stores the candidate.  (Single-thread trials, GYM_FLAG_RUN_SINGLE or more than 32
+// trials: wavefront 0 alone, tail_candidate.)
 constexpr int TL_RC = 2;
 constexpr int TL_RING = 2 * TL_RC * (BLK / 2) * 3 * 2;   // doubles
 constexpr size_t tail_lds_bytes(int T) {
-    return TL_SPLIT ? sizeof(double) * ((size_t)3 * TL_STAGES * TL_PITCH + (size_t)2 * TL_STAGES * TL_GK + 4 +
-                                        (size_t)TL_RING + (size_t)T * TL_TST)
-                    : sizeof(double) * ((size_t)TL_STAGES * TL_PITCH + (size_t)(BLK / 4) * QX_DOUBLES +
-                                        (size_t)T * TL_TST);
+    return sizeof(double) * ((size_t)3 * TL_STAGES * TL_PITCH + (size_t)2 * TL_STAGES * TL_GK + 4 +
+                             (size_t)TL_RING + (size_t)T * TL_TST);
 }
-// the sweep of lane l at iterate cb: K row 1, cg and sigma1 of every stage (global, and staged in tst); returns dJ,
-// max|sigma|
-template <bool U0Z, bool RL>
-__device__ __forceinline__ void tail_sweep(double* lin, double* xq, double* tst, int lane, int64_t l, int cb,
-                                           double& dJ_out, double& smax_out) {
-    const targs_t R = tail_args();
-    const int T = R->N - 1;
-    const int64_t Bp = R->Bp;
-    const double2* x = R->x[cb];
-    const double* u = R->u[cb];
-    const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
-    const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
-    const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
-    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
-    const char* Kb = reinterpret_cast<const char*>(R->K1);
-    const char* Cb = reinterpret_cast<const char*>(R->cs);
-    const double g0 = R->a.gamma0;
-    const double twoR1 = R->w.twoR1, iG00 = R->w.iG00, dt = R->m.h;   // loop-invariant (no kernarg reloads)
-    Sweep<false> S(R->w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
-    QuadSweep<U0Z> Q(R->w, lane, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
-    double* X = xq + (lane >> 2) * QX_DOUBLES;
-    for (int tb = T - 1; tb >= 0; tb -= TL_STAGES) {
-        const int t = tb - lane;   // this thread's stage of the pass
-        if (t >= 0) {
-            const double2 xa = x[wix(t, 0, 2, l, Bp)], xb = x[wix(t, 1, 2, l, Bp)];
-            const double u0 = U0Z ? 0.0 : u[pix(t, 0, 2, l, Bp)], u1 = u[pix(t, 1, 2, l, Bp)];
-            const KArgs ka = kernarg_consts();
-            const gym::Jac J = gym::jacobian(ka.m, xa.x, xa.y, xb.x, xb.y, u1);
-            const Lin L = stage_lin<U0Z>(ka.m, ka.w, J, xa, xb, u0, u1, xr + 4 * t, ur + 2 * t);
-            double* s = lin + lane * TL_PITCH;
-            s[0] = L.A20; s[1] = L.A21; s[2] = L.A22; s[3] = L.A23;
-            s[4] = L.A30; s[5] = L.A31; s[6] = L.A32; s[7] = L.A33;
-            s[8] = L.bd2; s[9] = L.bd3; s[10] = L.q0; s[11] = L.q1;
-            s[12] = L.q2; s[13] = L.q3; s[14] = L.r0; s[15] = L.r1;
-            s[16] = xa.x; s[17] = xa.y; s[18] = xb.x; s[19] = xb.y; s[20] = u1;
-            tst[t * TL_TST + 6] = u0;
-        }
-        __syncthreads();
-        const int n = tb + 1 < TL_STAGES ? tb + 1 : TL_STAGES;
-        for (int i = 0; i < n; ++i) {   // every thread runs the recursion (the same bits); thread 0 stores
-            const double* s = lin + i * TL_PITCH;
-            double k0, k1, k2, k3, s0, s1;
-            if (GYM_TAIL_QUAD) {
-                Q.step(twoR1, iG00, s, dt, X, k0, k1, k2, k3, s0, s1);
-            } else {
-                const KArgs ka = kernarg_consts();
-                const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
-                            s[10], s[11], s[12], s[13], s[14], s[15], dt};
-                S.step_lin<U0Z>(ka.w, L, k0, k1, k2, k3, s0, s1);
-            }
-            const double2 xa = make_double2(s[16], s[17]), xb = make_double2(s[18], s[19]);
-            if (lane == 0) {
-                const int ts = tb - i;
-                const double cg = stage_cg(xa, xb, s[20], g0, k0, k1, k2, k3, s1);
-                double* q = tst + ts * TL_TST;
-                q[0] = k0; q[1] = k1; q[2] = k2; q[3] = k3; q[4] = cg; q[5] = s1;
-                const auto rC = rsrc(Cb + (int64_t)ts * row);
-                const auto rK = rsrc(Kb + (int64_t)ts * (2 * (int64_t)row));
-                bst2(rK, o2, 0, k0, k1);
-                bst2(rK, o2, WROW, k2, k3);
-                bst1(rC, o1, 0, cg);
-                bst1(rC, o1, plane, s1);
-            }
-        }
-        __syncthreads();
-    }
-    dJ_out = GYM_TAIL_QUAD ? Q.dJ : S.dJ;
-    smax_out = GYM_TAIL_QUAD ? Q.smax : S.smax;
-}
-
-// GYM_TAIL_SPLIT: the sweep of lane l on two wavefronts.  Pass j covers stages T-1-64j down to T-64-64j.  Between
+// The sweep of lane l at iterate cb on two wavefronts: K row 1, cg and sigma1 of every stage (global, and staged in
+// tst).  Pass j covers stages T-1-64j down to T-64-64j.  Between
 // workgroup barriers j and j+1, wavefront 0 runs the matrix half over pass j (linearisations lin3[j % 3], gain rows
 // into gk2[j & 1]) while wavefront 1 runs the vector half over pass j - 1 (its linearisations and gain rows, K row
 // 1 / cg / sigma1 stored and staged in tst) and then evaluates pass j + 1's linearisations.  Every thread of a
@@ -2858,11 +2322,9 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
             tst[t * TL_TST + 6] = u0;
         }
     };
-#if GYM_TAIL_SWEEP_VGPR
     KW wv = R->w;                          // the Riccati halves' weights in VGPRs: no per-stage kernel-argument loads
     gym::in_vgpr(wv.twoQ[0]); gym::in_vgpr(wv.twoQ[1]); gym::in_vgpr(wv.twoQ[2]); gym::in_vgpr(wv.twoQ[3]);
     gym::in_vgpr(wv.twoR1); gym::in_vgpr(wv.iG00);
-#endif
     if (wave == 1) linearise(0);
     __syncthreads();
     for (int j = 0; j <= np; ++j) {
@@ -2874,11 +2336,7 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                 double* G = gk2 + (j & 1) * TL_STAGES * TL_GK;
                 for (int i = 0; i < n; ++i) {
                     const double* s = L3 + i * TL_PITCH;
-#if GYM_TAIL_SWEEP_VGPR
                     const KW& kw = wv;
-#else
-                    const KW kw = kernarg_consts().w;
-#endif
                     const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
                                 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dt};   // q, r: the vector half's
                     double k0, k1, k2, k3, G11, iG;
@@ -2900,11 +2358,7 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                     const double* s = L3 + i * TL_PITCH;
                     const double* g = G + i * TL_GK;
                     const double k0 = g[0], k1 = g[1], k2 = g[2], k3 = g[3];
-#if GYM_TAIL_SWEEP_VGPR
                     const KW& kw = wv;
-#else
-                    const KW kw = kernarg_consts().w;
-#endif
                     const Lin L{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
                                 s[10], s[11], s[12], s[13], s[14], s[15], dt};
                     double s0, s1;
@@ -2931,11 +2385,10 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
     }
 }
 
-// Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) into virtual lane v of the
-// scratch, its streams from the staging tst; returns the candidate's cost
-template <bool U0Z, bool RL, bool PAIR>
-__device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, int cb, int c, double g, int64_t v,
-                                                 bool odd) {
+// Armijo trial c of lane l (step size g; c = 0: the first trial's offset form) on one thread into virtual lane v of
+// the scratch, its streams from the staging tst; returns the candidate's cost
+template <bool U0Z, bool RL>
+__device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, int cb, int c, double g, int64_t v) {
     const targs_t R = tail_args();
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
@@ -2948,13 +2401,10 @@ __device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, i
     const double gamma0 = R->a.gamma0, dg = g - gamma0;
     const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
     double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
-    // PAIR: the candidate's chain on a lane pair (gym::rk4_pair, bit-identical to rk4); the even lane stores
-    // (th1, th2) and the controls, the odd lane (w1, w2)
-    const bool st_a = !PAIR || !odd, st_b = !PAIR || odd;
     {
         const auto rX = rsrc(Xs);
-        if (st_a) bst2(rX, v2, 0, n0, n1);
-        if (st_b) bst2(rX, v2, WROW, n2, n3);
+        bst2(rX, v2, 0, n0, n1);
+        bst2(rX, v2, WROW, n2, n3);
     }
     double J = 0.0;
     const gym::PolyRegs pk = gym::poly_vgprs();
@@ -2974,26 +2424,21 @@ __device__ __forceinline__ double tail_candidate(const double* tst, int64_t l, i
         const double f0 = U0Z ? 0.0 : v0 - urt.v[0], f1 = u1 - urt.v[1];
         const KArgs kc = kernarg_consts();
         J = stage_cost<U0Z>(J, kc.w.Q, kc.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
-        if (st_a) {
+        {
             const auto rO = rsrc(Us + (int64_t)t * srow);
             if (!U0Z) bst1(rO, v1o, 0, v0);
             bst1(rO, v1o, splane, u1);
         }
-        if (PAIR && GYM_TAIL_NEAR)
-            gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
-        else if (PAIR)
-            gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
-        else
-            gym::rk4(m, n0, n1, n2, n3, u1, pk);
+        gym::rk4(m, n0, n1, n2, n3, u1, pk);
         const auto rX = rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow));
-        if (st_a) bst2(rX, v2, 0, n0, n1);
-        if (st_b) bst2(rX, v2, WROW, n2, n3);
+        bst2(rX, v2, 0, n0, n1);
+        bst2(rX, v2, WROW, n2, n3);
     }
     const Row<4> xrT = ref_row<4, RL>(xr, T);
     return J + xcost(ka.w.QT, n0, n1, n2, n3, xrT.v);
 }
 
-// TL_SPLIT, wavefront 0: the RK4 chain of Armijo trial c on the lane pair (2c, 2c + 1) -- the offset-form feedback
+// Wavefront 0: the RK4 chain of Armijo trial c on the lane pair (2c, 2c + 1) -- the offset-form feedback
 // and gym::rk4_pair, exactly tail_candidate's chain -- handing each stage's state and control to wavefront 1 (ring
 // [chunk & 1][stage in chunk][trial][(th1, th2) | (w1, w2) | (u1, -)]).  Chunk cc between barriers cc and cc + 1.
 typedef double2 (*tring_t)[TL_RC][BLK / 2][3];
@@ -3006,18 +2451,12 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
     const double dg = g - R->a.gamma0;
     const double2 xa = R->x[cb][wix(0, 0, 2, l, Bp)], xb = R->x[cb][wix(0, 1, 2, l, Bp)];
     double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
-#if GYM_TAIL_CHAIN_VGPR
     // every Horner coefficient and the model in VGPRs across the chain's loop (as k_nt_run2's trial chain)
     const gym::PolyRegs pk = gym::poly_vgprs_all();
     Dyn m = kernarg_consts().m;
     gym::in_vgpr(m.b); gym::in_vgpr(m.d); gym::in_vgpr(m.a2b); gym::in_vgpr(m.bb); gym::in_vgpr(m.dad);
     gym::in_vgpr(m.g1); gym::in_vgpr(m.g2); gym::in_vgpr(m.f1); gym::in_vgpr(m.f2); gym::in_vgpr(m.h);
     gym::in_vgpr(m.h2); gym::in_vgpr(m.h6);
-#else
-    const gym::PolyRegs pk = gym::poly_vgprs();
-    const KArgs ka = kernarg_consts();
-    const Dyn m = ka.m;
-#endif
     const int nch = (T + TL_RC - 1) / TL_RC;
     const int tc = c < BLK / 2 ? c : 0;
     for (int cc = 0; cc < nch; ++cc) {
@@ -3030,10 +2469,7 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
                 const double y = trial_u1(k0, k1, q[4], n0, n1, n2, n3);   // cg + K1 x_new: trial 1's value
                 const double ysig = __builtin_fma(dg, q[5], y);             // trial_u1_sig's value
                 const double u1 = c == 0 ? y : ysig;
-                if (GYM_TAIL_NEAR)
-                    gym::rk4_pair_fast<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
-                else
-                    gym::rk4_pair<GYM_RUN2_PAIR_VOP3>(m, odd, n0, n1, n2, n3, u1, pk);
+                gym::rk4_pair_fast<true>(m, odd, n0, n1, n2, n3, u1, pk);   // branch-free near path, as k_nt_run2
                 double2* r = ring[cc & 1][j][tc];
                 if (odd) r[1] = make_double2(n2, n3);
                 else { r[0] = make_double2(n0, n1); r[2] = make_double2(u1, 0.0); }
@@ -3044,7 +2480,7 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
     __syncthreads();                       // the helper's last chunk
 }
 
-// TL_SPLIT, wavefront 1, lane c (< max_ls): trial c's cost (stage costs in stage order, as tail_candidate) and its
+// Wavefront 1, lane c (< max_ls): trial c's cost (stage costs in stage order, as tail_candidate) and its
 // candidate trajectory into virtual lane v of the scratch; returns J.  Chunk cc between barriers cc + 1 and cc + 2.
 template <bool U0Z, bool RL>
 __device__ __forceinline__ double tail_trial_helper(const double* tst, tring_t ring, int64_t l, int cb, int c, double g,
@@ -3109,16 +2545,15 @@ __device__ unsigned long long g_tail_trace[4096][4];
 #endif
 template <bool U0Z, bool RL, bool PAIR>
 __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
-    extern __shared__ double tail_lds[];          // tail_lds_bytes(T): linearisations, quad exchange, trial staging
-    // TL_SPLIT: lin3 (3 passes) | gk2 (2 passes of gain rows) | shd (dJ, max|sigma|, the decision) | tst
+    extern __shared__ double tail_lds[];          // tail_lds_bytes(T)
+    // lin3 (3 passes) | gk2 (2 passes of gain rows) | shd (dJ, max|sigma|, the decision) | ring | tst
     double* lin = tail_lds;
-    double* xq = lin + TL_STAGES * TL_PITCH;
     double* gk2 = lin + 3 * TL_STAGES * TL_PITCH;
     double* shd = gk2 + 2 * TL_STAGES * TL_GK;
-    const tring_t ring = reinterpret_cast<tring_t>(shd + 4);   // TL_SPLIT with PAIR: the trials' hand-off
-    double* tst = TL_SPLIT ? shd + 4 + TL_RING : xq + (BLK / 4) * QX_DOUBLES;
+    const tring_t ring = reinterpret_cast<tring_t>(shd + 4);   // PAIR: the trials' hand-off
+    double* tst = shd + 4 + TL_RING;
     const int lane = threadIdx.x & (BLK - 1);
-    const int wave = threadIdx.x / BLK;           // TL_SPLIT: 0 the matrix half and the trials, 1 the vector half
+    const int wave = threadIdx.x / BLK;           // 0 the matrix half and the trials, 1 the vector half
     const int64_t l = tail_args()->list[blockIdx.x];
     int st = tail_args()->status[l];
     unsigned long long acc[4] = {0, 0, 0, 0};   // GYM_TAIL_TRACE only
@@ -3127,13 +2562,9 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
         double dJ, sm;
         unsigned long long tt = R2T_NOW();
         ++acc[3];
-        if (TL_SPLIT) {
-            tail_sweep_split<U0Z, RL>(lin, gk2, shd, tst, wave, lane, l, cb);   // ends at a workgroup barrier
-            dJ = shd[0];
-            sm = shd[1];
-        } else {
-            tail_sweep<U0Z, RL>(lin, xq, tst, lane, l, cb, dJ, sm);
-        }
+        tail_sweep_split<U0Z, RL>(lin, gk2, shd, tst, wave, lane, l, cb);   // ends at a workgroup barrier
+        dJ = shd[0];
+        sm = shd[1];
         acc[0] += R2T_NOW() - tt;
         tt = R2T_NOW();
         {
@@ -3146,17 +2577,17 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
         }
         __syncthreads();   // the staged trial inputs (LDS) complete
         const int max_ls = tail_args()->a.max_ls;
-        // TL_SPLIT with lane pairs: wavefront 0 runs the trials' chains (trial c on lanes 2c, 2c + 1), wavefront 1
-        // (lane c: trial c) their costs, stores and Armijo tests; otherwise wavefront 0 does all of it
-        constexpr bool HELPER = TL_SPLIT && PAIR;
-        const int dec = HELPER ? 1 : 0;             // the wavefront holding the decisions
-        const int cand = (PAIR && !(HELPER && wave == 1)) ? lane >> 1 : lane;   // this thread's trial
+        // PAIR: wavefront 0 runs the trials' chains (trial c on lanes 2c, 2c + 1), wavefront 1 (lane c: trial c) their
+        // costs, stores and Armijo tests; otherwise wavefront 0 does all of it, one trial per thread
+        const int dec = PAIR ? 1 : 0;               // the wavefront holding the decisions
+        const bool helper_wave = PAIR && wave == 1;  // lane c: trial c's cost
+        const int cand = (PAIR && !helper_wave) ? lane >> 1 : lane;   // this thread's trial
         const int64_t v = (int64_t)blockIdx.x * max_ls + cand;
         double g = tail_args()->a.gamma0;
         for (int q = 0; q < cand && q < max_ls; ++q) g *= tail_args()->a.beta;   // gamma_i *= beta (:365)
         bool ok = false;
         double Jn = 0.0;
-        if (HELPER) {
+        if (PAIR) {
             if (wave == 0) {
                 tail_trial_chain<U0Z, RL>(tst, ring, l, cb, cand, g, lane & 1);
             } else {
@@ -3165,22 +2596,20 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
                 ok = cand < max_ls && Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
             }
         } else if (cand < max_ls && wave == 0) {
-            Jn = tail_candidate<U0Z, RL, PAIR>(tst, l, cb, cand, g, v, lane & 1);
+            Jn = tail_candidate<U0Z, RL>(tst, l, cb, cand, g, v);
             const targs_t R = tail_args();
             ok = Jn < R->cost[l] + R->a.c * g * dJ;   // strict Armijo test (:361)
         }
         const unsigned long long okm = __ballot(ok);
         acc[1] += R2T_NOW() - tt;
         tt = R2T_NOW();
-        // the first accepted trial, in order (PAIR without the helper: both lanes of a pair hold the same decision);
-        // TL_SPLIT: handed from the deciding wavefront to the other so that both leave the iteration loop together
-        int first = okm ? (__ffsll((long long)okm) - 1) / ((PAIR && !HELPER) ? 2 : 1) : -1;
+        // the first accepted trial, in order, handed from the deciding wavefront to the other so that both leave the
+        // iteration loop together
+        int first = okm ? __ffsll((long long)okm) - 1 : -1;
         lane_fence();   // the candidates' scratch stores, before the copy reads them
-        if (TL_SPLIT) {
-            if (wave == dec && lane == 0) shd[2] = (double)first;
-            __syncthreads();
-            first = (int)shd[2];
-        }
+        if (wave == dec && lane == 0) shd[2] = (double)first;
+        __syncthreads();
+        first = (int)shd[2];
         const int nr = first >= 0 ? first + 1 : max_ls;
         if (first >= 0 && wave == 0) {   // the accepted candidate becomes the lane's next iterate (buffer cb ^ 1)
             const targs_t R = tail_args();
@@ -3215,7 +2644,7 @@ __global__ __launch_bounds__(TL_THREADS, 1) void k_nt_tail(TailArgs args) {
                 }
             }
         }
-        const int src = (first >= 0 ? first : 0) * ((PAIR && !HELPER) ? 2 : 1);
+        const int src = first >= 0 ? first : 0;
         const double Jf = __shfl(Jn, src);
         const double gf = __shfl(g, src);
         if (lane == 0 && wave == dec) {
@@ -3422,9 +2851,7 @@ __global__ __launch_bounds__(BLK) void k_fill_states(Dyn m, double2* __restrict_
 // average duration is the roofline's denominator.  The short post-trial kernels (candidates, retry, statistics,
 // sigma1 re-run: five per phase) keep one sampled pair per kind and collect: an event pair around each of them
 // lengthened the phase-to-phase gap from ~28 to ~73 us in the rocprofv3 trace (+1-2% per solve).
-#ifndef GYM_TIMING_POOL_KINDS
-#define GYM_TIMING_POOL_KINDS ((1 << 0) | (1 << 1) | (1 << 5) | (1 << 6) | (1 << 8) | (1 << 9))
-#endif
+constexpr int TIMING_POOL_KINDS = (1 << 0) | (1 << 1) | (1 << 5) | (1 << 6) | (1 << 8) | (1 << 9);
 struct TimedLaunch {  // records a start/stop event pair around one launch: a pool pair, else the kind's free slot
     gym_timing* t;
     int kind;
@@ -3432,7 +2859,7 @@ struct TimedLaunch {  // records a start/stop event pair around one launch: a po
     int slot;            // pool index, -1: the kind's sampled pair, -2: not timed
     TimedLaunch(gym_timing* t_, int kind_, hipStream_t s_) : t(t_), kind(kind_), s(s_), slot(-2) {
         if (!t) return;
-        if (((GYM_TIMING_POOL_KINDS >> kind) & 1) && t->pool_used < GYM_TIMING_POOL && t->pool_ev[0]) {
+        if (((TIMING_POOL_KINDS >> kind) & 1) && t->pool_used < GYM_TIMING_POOL && t->pool_ev[0]) {
             slot = t->pool_used++;
             t->pool_kind[slot] = kind;
             (void)hipEventRecord((hipEvent_t)t->pool_ev[2 * slot], s);
@@ -3665,14 +3092,11 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
 }
 
 // Grid caps of the post-trial kernels (grid-stride over the retry list; any cap is correct).  They launch every
-// phase, also when no lane rejected trial 1 (the device-side count is not known to the host); measurement
-// variants lower them.
-#ifndef GYM_POST_CAP
-#define GYM_POST_CAP 2048
-#endif
-#ifndef GYM_CAND_CAP
-#define GYM_CAND_CAP 4096
-#endif
+// phase, also when no lane rejected trial 1 (the device-side count is not known to the host).  Lower caps (256 /
+// 64) measured the same at 262,144 lanes and 2% slower on the stress start: the gap between phases is
+// launch latency, not workgroup dispatch.
+constexpr int64_t POST_CAP = 2048;
+constexpr int64_t CAND_CAP = 4096;
 static void launch_post_trial(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                               const SolverCtl& c, const TrialIO& io, Range rg, int32_t* counter, double* stats_out,
                               const double* other, double* total, hipStream_t st, bool sigma_streamed = false) {
@@ -3683,18 +3107,18 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
     if (a->max_ls > 1 && n > 0) {
         if (!sigma_streamed) {   // the lanes that reject trial 1 need sigma1: re-run their sweep into its plane
             TimedLaunch tl(b->timing, 7, st);
-            hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, GYM_POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
+            hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_sigma), dim3(grid_for(n, BLK, POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
                                kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
                                (const int32_t*)nullptr, -1, b->B, b->Bp, b->N);
         }
         {
             TimedLaunch tl(b->timing, 2, st);
-            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, GYM_CAND_CAP);
+            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, CAND_CAP);
             hipLaunchKernelGGL(CAND_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
                                b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, GYM_POST_CAP)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, POST_CAP)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
                            b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
                            b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
     }
@@ -3794,7 +3218,7 @@ int gym_newton_run(const gym_model* m, const gym_weights* w, const gym_armijo* a
                    int32_t k1, void* s) {
     // GYM_FLAG_SIGMA_STREAM with the four-wavefront kernel: one iteration per launch, its sweep storing sigma1, the
     // lanes that reject trial 1 finished by the serial schedule's parallel candidates and accepted re-run
-    const bool ext = (b->flags & GYM_FLAG_SIGMA_STREAM) && !(b->flags & GYM_FLAG_RUN_SINGLE) && R2SPLIT;
+    const bool ext = (b->flags & GYM_FLAG_SIGMA_STREAM) && !(b->flags & GYM_FLAG_RUN_SINGLE);
     if (bad_iter_args(m, w, a, b) || k0 < 0 || k1 < k0 || (b->flags & GYM_FLAG_X_CKPT) || (ext && k1 > k0 + 1))
         return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;

@@ -18,12 +18,6 @@
 #define GYM_HORNER_VOP3 1   // three-address Horner steps (acrobot_device.hpp): no per-step constant copies
 #endif
 #include "acrobot_device.hpp"
-#ifndef GYM_TRACK_DYN_VGPR
-#define GYM_TRACK_DYN_VGPR 1
-#endif
-#ifndef GYM_TRACK_NEAR
-#define GYM_TRACK_NEAR 1   // the pair rollout's RK4 step branch-free on the near path (gym::rk4_pair_fast)
-#endif
 #include "gymnast_acrobot.h"
 
 using gym::Dyn;
@@ -390,12 +384,8 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
 // latency-bound rollout less (cfg 5: 426 -> 412 us, tools/rollout_probe.py; staging the steps in LDS to write
 // whole-trajectory runs was slower, 458 us: LDS traffic shares lgkmcnt with the per-step scalar loads)
 __device__ __forceinline__ void st_nt2(double2* p, double a, double b) {
-#ifdef GYM_TRACK_PLAIN_STORES   // measurement variant: the default cache policy
-    *p = make_double2(a, b);
-#else
     typedef double d2v __attribute__((ext_vector_type(2)));
     __builtin_nontemporal_store(d2v{a, b}, reinterpret_cast<d2v*>(p));
-#endif
 }
 
 // k_track_rollout with each trajectory on a lane pair (gym::rk4_pair): 2B threads, 128 B... of one lane's rows
@@ -422,13 +412,11 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
 #pragma unroll
     for (int q = 0; q < 4; ++q) r[q] = x_ff[q];
     f[0] = u_ff[0]; f[1] = u_ff[1];
-    const gym::PolyRegs pk = GYM_TRACK_NEAR ? gym::poly_vgprs_all() : gym::poly_vgprs();
-    Dyn dm = m;                            // GYM_TRACK_DYN_VGPR: the model in VGPRs across the step loop
-    if (GYM_TRACK_DYN_VGPR) {
-        gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
-        gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
-        gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
-    }
+    const gym::PolyRegs pk = gym::poly_vgprs_all();   // every Horner coefficient in VGPRs
+    Dyn dm = m;                            // the model in VGPRs across the step loop
+    gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+    gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+    gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
         const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
@@ -442,10 +430,7 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
             f[0] = u_ff[2 * (t + 1)]; f[1] = u_ff[2 * (t + 1) + 1];
         }
         if (!odd) st_nt2(ul + t, v0, v1);
-        if (GYM_TRACK_NEAR)
-            gym::rk4_pair_fast(dm, odd, n0, n1, n2, n3, v1, pk);
-        else
-            gym::rk4_pair(m, odd, n0, n1, n2, n3, v1, pk);
+        gym::rk4_pair_fast(dm, odd, n0, n1, n2, n3, v1, pk);   // branch-free near path (gym::rk4_pair_fast)
         if (odd) st_nt2(xl + 2 * (t + 1), n2, n3);
         else st_nt2(xl + 2 * (t + 1), n0, n1);
     }
