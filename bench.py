@@ -144,8 +144,12 @@ def mpc_line(a, B, steps, warmup, cpu_lanes):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     ctrl_steps = B * (N - 1)
-    # per-kernel times (HIP events on the engine's stream = torch's current stream)
+    # per-kernel times (HIP events on the engine's stream = torch's current stream).  The stream is kept busy
+    # (torch.cuda._sleep) while the host enqueues the events and the two launches, so each interval is the kernel's
+    # execution, not the host's Python time between two records on an idle GPU (round 3's line included it:
+    # 0.111 ms for a 77 us gains kernel)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    torch.cuda._sleep(2_000_000)
     ev[0].record()
     K0, QT = tt.mpc_gains(xrd, urd, a.horizon)
     ev[1].record()
@@ -190,11 +194,11 @@ class NewtonLeg:
     """One timed configuration of the batched solver on this rank: ``total`` global lanes of the bench workload,
     this rank's contiguous shard, the schedule chosen on the largest shard (identical on every rank)."""
 
-    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None):
+    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None, spread=None):
         from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
         self.rank, self.world = gd.rank_world()
         self.total = int(total)
-        self.x0_all = make_x0(self.total, spread=a.spread)
+        self.x0_all = make_x0(self.total, spread=a.spread if spread is None else spread)
         lo, hi = gd.shard_range(self.total, self.rank, self.world)
         sched = {"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule]
         self.solver = BatchedNewtonSolver(
@@ -206,7 +210,8 @@ class NewtonLeg:
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
-        self.reduce = gd.make_reduce_stats()
+        base = gd.make_reduce_stats()
+        self.reduce = gd.TimedReduce(base) if base is not None else None
         self.a, self.gd = a, gd
 
     def run(self, steps: int, warmup: int):
@@ -215,6 +220,8 @@ class NewtonLeg:
         for _ in range(warmup):
             solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
         solver.reset_timing()
+        if self.reduce is not None:
+            self.reduce.reset()
         gd.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -228,8 +235,13 @@ class NewtonLeg:
             compactions += res.compactions
             lowocc_its += res.lowocc_lane_iterations
         torch.cuda.synchronize()
+        local = time.perf_counter() - t0       # this rank's own time, before waiting for the others
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
+        red = self.reduce
+        self.rank_records = gd.gather_floats([local, lane_its, red.reduce_s if red else 0.0,
+                                              red.readback_s if red else 0.0, red.calls if red else 0,
+                                              res.iterations if res is not None else 0])
         self.res, self.lane_its, self.steps, self.tail_lane_its = res, lane_its, steps, tail_its
         self.compactions = compactions
         self.lowocc_lane_its = lowocc_its
@@ -295,6 +307,21 @@ class NewtonLeg:
         import torch
         self.solver = self.res = self.x0_dev = None
         torch.cuda.empty_cache()
+
+
+def outcome_record(res) -> dict:
+    """Per-lane outcomes of a solve: statuses, iteration range, rollouts and the per-lane extra Armijo trials
+    (rollouts beyond one per iteration) binned."""
+    st = res.status.cpu().numpy()
+    extra = (res.n_rollouts - res.n_iter).cpu().numpy()
+    edges = [0, 1, 2, 4, 8, 16, 32, 1 << 30]
+    return {"converged": int((st == 1).sum()), "ls_failed": int((st == 2).sum()), "max_iters": int((st == 3).sum()),
+            "lane_iters_min_max": [int(res.n_iter.min().item()), int(res.n_iter.max().item())],
+            "outer_iterations": int(res.iterations), "rollouts": int(res.n_rollouts.sum().item()),
+            "lanes_that_backtracked": int((res.n_rollouts > res.n_iter).sum().item()),
+            "extra_trials_histogram": {
+                (f"{lo}" if hi == lo + 1 else f"{lo}-{hi - 1}" if hi < (1 << 30) else f">={lo}"):
+                    int(((extra >= lo) & (extra < hi)).sum()) for lo, hi in zip(edges[:-1], edges[1:])}}
 
 
 def pmc_traffic(dom: str):
@@ -372,11 +399,12 @@ def main():
                     help="newton: the north-star metric (cfg 3 per GPU, weak scaling); cfg4: 1,048,576 lanes "
                          "strong-scaled over the ranks; mpc: BASELINE cfg 5; stress: the cfg 3 batch with "
                          "th ~ U(+-1.5) (SURVEY 8(d)'s stress variant: backtracking and Armijo failures)")
-    ap.add_argument("--extra-legs", default="cfg4,general,cfg2,mpc",
+    ap.add_argument("--extra-legs", default="cfg4,general,cfg2,mpc,stress",
                     help="comma list of secondary timed legs reported inside the same JSON line (newton "
                          "workload): cfg4 = 1,048,576 lanes strong-scaled over the ranks; general = the same "
                          "workload on the general (tau1-streaming) kernels, N=1 only; cfg2 = BASELINE cfg 2 "
-                         "(4,096 lanes, N=1 only); mpc = BASELINE cfg 5 (N=1 only); '' for none")
+                         "(4,096 lanes, N=1 only); mpc = BASELINE cfg 5 (N=1 only); stress = SURVEY 8(d)'s "
+                         "stress variant (th ~ U(+-1.5), N=1 only); '' for none")
     ap.add_argument("--extra-steps", type=int, default=2, help="timed solves of each extra leg (1 warmup)")
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
@@ -521,6 +549,22 @@ def main():
         out["roofline"].update({k: v for k, v in roof.items() if k not in out["roofline"]})
         out["kernels"] = kern
     out["schedule"] = main_leg.schedule()
+    if world > 1:
+        # per-rank diagnostics of the main leg: a sub-linear scaling curve then says whether stragglers (spread of
+        # the ranks' own elapsed times and lane-iterations), the statistics all-reduce or its read-back is the cause
+        recs = main_leg.rank_records
+        el = [r[0] for r in recs]
+        out["dist"].update({
+            "rank_elapsed_s": el, "rank_elapsed_min_max": [min(el), max(el)],
+            "rank_lane_iterations": [int(r[1]) for r in recs],
+            "rank_outer_iterations_last_step": [int(r[5]) for r in recs],
+            "rank_reduce_host_s": [r[2] for r in recs], "rank_readback_host_s": [r[3] for r in recs],
+            "allreduce_calls_per_step": int(recs[0][4]) // max(a.steps, 1),
+            "allreduce_8xf64_us": gd.allreduce_latency_us(),
+            "note": "rank_elapsed_s: each rank's own timed region before the closing barrier (max = ms_per_step x "
+                    "steps); rank_reduce_host_s: host time inside the statistics all-reduce calls; "
+                    "rank_readback_host_s: host time reading the reduced statistics back (includes waiting for the "
+                    "queued iterations); allreduce_8xf64_us: one statistics all-reduce, measured after the run"})
     if parity is not None:
         out["parity"] = parity
     res = None
@@ -565,6 +609,31 @@ def main():
             "roofline": None if r2 is None else {k: r2[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
             "note": "BASELINE cfg 2: 4,096 lanes on one GPU (64 wavefronts of lanes on 1,024 SIMDs: latency-bound, "
                     "the persistent schedule); --batch 4096 makes it the main line"}
+        leg.free()
+    if "stress" in legs and world == 1:
+        # SURVEY 8(d)'s stress variant: the cfg 3 batch with th ~ U(+-1.5): backtracking, Armijo failures and a
+        # straggler tail; the automatic schedule (pipelined -> lane compaction / low-occupancy regime -> tail)
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, spread=1.5).run(a.extra_steps, 1)
+        ks, rs = leg.kernel_report(N)
+        sv = leg.solver
+        out["stress"] = {
+            "value": leg.value, "unit": "Newton iterations/s", "lanes": total, "steps": a.extra_steps, "warmup": 1,
+            "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
+            "rollouts_per_s": leg.rollouts_all / leg.elapsed,
+            "roofline": None if rs is None else {k: rs[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
+            "straggler_tail": {"launches_per_step": sv.launches["tail"] / a.extra_steps,
+                               "share_of_lane_iterations": leg.tail_lane_its / max(leg.lane_its, 1),
+                               "seconds_per_step": None if not ks or "tail" not in ks else
+                               ks["tail"]["avg_ms"] * ks["tail"]["launches"] / 1e3 / a.extra_steps},
+            "low_occupancy": {"from_iteration": sv.serial_switch_at, "compactions_per_step":
+                              leg.compactions / a.extra_steps,
+                              "share_of_lane_iterations": leg.lowocc_lane_its / max(leg.lane_its, 1)},
+            "outcomes": outcome_record(leg.res),
+            "note": "SURVEY 8(d) stress variant: x0 = [th1, th2, 0, 0], th ~ U(+-1.5) (default_rng(0)), task-2 "
+                    "settings, solved to convergence; the roofline is the phase kernel's over the lane-iterations "
+                    "the phases ran (the tail and the low-occupancy regime are reported apart); decisions pinned "
+                    "lane by lane against the C oracle (tests/test_gpu_stress.py)"}
         leg.free()
     if "mpc" in legs and world == 1:
         m = mpc_line(a, 8192, max(a.extra_steps, 3), 1, 0)

@@ -335,6 +335,18 @@ __global__ void k_lq_forward(const double* __restrict__ A, const double* __restr
     X[4 * (L - 1)] = x[0]; X[4 * (L - 1) + 1] = x[1]; X[4 * (L - 1) + 2] = x[2]; X[4 * (L - 1) + 3] = x[3];
 }
 
+// The tracking feedback u = u_ff + K (x - x_ff) (simulate_tracking :210, the MPC loop's u = K x0 + u_ref :50) with
+// FMA contraction inside the expression only: the frontend then fuses the same product of every sum in every kernel
+// and code context.  Under the file's default -ffp-contract=fast the backend chose per context: a pair rollout
+// unrolled by two with double-buffered rows (round 3) fused k1 d1 instead of k0 d0 in its second step and lost
+// bitwise equality with the single-lane kernel (tools/mpc_rowbuf_probe.py, profiles/r04/mpc_rowbuf/).
+__device__ __forceinline__ void track_feedback(const double* k, const double* f, double d0, double d1, double d2,
+                                               double d3, double& v0, double& v1) {
+#pragma clang fp contract(on)
+    v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
+    v1 = f[1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+}
+
 // Batched closed-loop tracking simulation (simulate_tracking :206-216; MPC loop :43-60):
 //   u_t = u_ff[t] + K[t] (x_t - x_ff[t]),  x_{t+1} = RK4(x_t, u_t)
 // x0 (B,4); shared x_ff (N,4), u_ff (T,2), K (T,2,4); outputs lane-major x (B,N,4), u (B,T,2).  Each lane is a
@@ -362,8 +374,8 @@ __global__ __launch_bounds__(64) void k_track_rollout(Dyn m, const double* __res
     const gym::PolyRegs pk = gym::poly_vgprs();   // minimax coefficients held in VGPRs (acrobot_device.hpp)
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
-        const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
-        const double v1 = f[1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+        double v0, v1;
+        track_feedback(k, f, d0, d1, d2, d3, v0, v1);
         if (t + 1 < T) {   // next step's shared operands, in flight during this step's RK4
             const double* kn = K + 8 * (t + 1);
 #pragma unroll
@@ -419,8 +431,8 @@ __global__ __launch_bounds__(64) void k_track_rollout_pair(Dyn m, const double* 
     gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
     for (int t = 0; t < T; ++t) {
         const double d0 = n0 - r[0], d1 = n1 - r[1], d2 = n2 - r[2], d3 = n3 - r[3];
-        const double v0 = f[0] + (((k[0] * d0 + k[1] * d1) + k[2] * d2) + k[3] * d3);
-        const double v1 = f[1] + (((k[4] * d0 + k[5] * d1) + k[6] * d2) + k[7] * d3);
+        double v0, v1;
+        track_feedback(k, f, d0, d1, d2, d3, v0, v1);
         if (t + 1 < T) {
             const double* kn = K + 8 * (t + 1);
 #pragma unroll

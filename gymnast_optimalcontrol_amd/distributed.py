@@ -97,6 +97,66 @@ def make_reduce_stats(group=None, force: bool = False):
     return reduce_stats
 
 
+class TimedReduce:
+    """A ``make_reduce_stats`` all-reduce with host-side accounting, for diagnosing a multi-GPU run: ``reduce_s``
+    accumulates the host time inside the collective call (enqueue on RCCL; the whole exchange on gloo) and
+    ``readback_s`` the host time of reading the reduced statistics back (it also waits for the iterations queued
+    before the collective, so it bounds the collective's share from above); ``calls`` counts the collectives.  It
+    returns the statistics on the host (the solver loops read them there at once), so the solve is unchanged."""
+
+    def __init__(self, reduce):
+        self.reduce = reduce
+        self.reduce_s = 0.0
+        self.readback_s = 0.0
+        self.calls = 0
+
+    def reset(self):
+        self.reduce_s = self.readback_s = 0.0
+        self.calls = 0
+
+    def __call__(self, st):
+        import time
+        t0 = time.perf_counter()
+        r = self.reduce(st)
+        t1 = time.perf_counter()
+        r = r.cpu() if isinstance(r, torch.Tensor) else r
+        t2 = time.perf_counter()
+        self.reduce_s += t1 - t0
+        self.readback_s += t2 - t1
+        self.calls += 1
+        return r
+
+
+def allreduce_latency_us(n: int = 200, group=None, force: bool = False) -> float | None:
+    """Average wall time of one 8 x fp64 SUM all-reduce (the solver's statistics message) issued back to back and
+    synchronised once, in microseconds; None without a collective."""
+    if not _collective(group, force):
+        return None
+    import time
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.zeros(8, dtype=torch.float64, device=dev)
+    for _ in range(10):
+        dist.all_reduce(t, group=group)
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    dist.barrier(group=group)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        dist.all_reduce(t, group=group)
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e6
+
+
+def gather_floats(values, group=None, force: bool = False) -> list:
+    """Every rank's list of host floats, in rank order, on every rank (one all-gather)."""
+    if not _collective(group, force):
+        return [list(map(float, values))]
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, list(map(float, values)), group=group)
+    return parts
+
+
 def barrier(group=None):
     if dist.is_available() and dist.is_initialized():
         dist.barrier(group=group)

@@ -370,3 +370,32 @@ def test_kernel_sources_carry_no_variant_switches():
                 seen |= set(re.findall(r"\bGYM_[A-Z0-9_]+", m.group(2)))
     assert seen <= allowed, sorted(seen - allowed)
     assert {"GYM_WAVE_TRACE", "GYM_RUN2_TRACE", "GYM_TAIL_TRACE"} <= seen
+
+
+def test_tracking_feedback_fuses_the_same_product_in_every_rollout():
+    """The tracking feedback u = u_ff + K (x - x_ff) is evaluated under contract(on) (track_feedback), so both
+    rollout kernels -- and any restructuring of them -- fuse the same product of every sum: in each feedback block
+    of the shipped library the separate v_mul multiplies d1 = x1 - x_ff1 and the next fma adds k0 d0, the
+    frontend's fmuladd(k0, d0, k1 d1).  Round 3's double-buffered pair rollout, compiled under -ffp-contract=fast,
+    fused k1 d1 in its second step instead and lost bitwise equality with the single-lane kernel
+    (tools/mpc_rowbuf_probe.py)."""
+    import re
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from gymnast_optimalcontrol_amd import _build
+    from mpc_rowbuf_probe import feedback_isa
+    blocks = feedback_isa(_build.build())
+    assert set(blocks) == {"single", "pair"} and all(blocks.values())
+    for kern, segs in blocks.items():
+        for seg in segs:
+            subs = [x for x in seg if re.match(r"v_add_f64 v\[\d+:\d+\], v\[\d+:\d+\], -s\[", x)]
+            assert len(subs) == 4, (kern, seg)
+            # d_j by the x_ff row's SGPR pair (r0 .. r3 at consecutive pairs)
+            d = {re.match(r"v_add_f64 (v\[\d+:\d+\])", x).group(1): int(re.search(r"-s\[(\d+):", x).group(1))
+                 for x in subs}
+            order = sorted(d, key=d.get)
+            muls = [x for x in seg if x.startswith("v_mul_f64")]
+            assert muls, (kern, seg)
+            for m in muls:
+                regs = re.findall(r"v\[\d+:\d+\]", m)[1:]
+                assert order[1] in regs, (kern, m, order)

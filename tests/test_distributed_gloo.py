@@ -286,3 +286,35 @@ def test_tail_switch_is_global_across_ranks(tmp_path):
     assert t0 == t1 and t0[0] == ("tail", 60, 76) and t0[-1][2] >= 100
     assert g[0]["calls"] == g[1]["calls"]                 # paired collectives
     assert g[0]["n_iter"] == [5, 60, 61] and g[1]["n_iter"] == [100, 7, 8, 9]
+
+
+def _timed_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+    from gymnast_optimalcontrol_amd import distributed as gd
+    gd.init_process_group(backend="gloo")
+    red = gd.TimedReduce(gd.make_reduce_stats())
+    outs = [red(torch.full((8,), float(rank + i), dtype=torch.float64)) for i in range(5)]
+    lat = gd.allreduce_latency_us(n=20)
+    recs = gd.gather_floats([red.reduce_s, red.readback_s, red.calls, lat])
+    if rank == 0:
+        np.save(out_path, np.array([[o.numpy() for o in outs], recs], dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_timed_reduce_accounts_host_time(tmp_path):
+    """bench.py's per-rank diagnostics (distributed.TimedReduce, allreduce_latency_us, gather_floats) on 2 gloo
+    ranks: the wrapped all-reduce returns the same sums on the host, counts its calls, and accumulates host time."""
+    out = str(tmp_path / "timed.npy")
+    mp.start_processes(_timed_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    outs, recs = np.load(out, allow_pickle=True)     # written by this test's own workers
+    for i, o in enumerate(outs):
+        np.testing.assert_array_equal(o, np.full(8, float(0 + i) + float(1 + i)))
+    assert len(recs) == 2
+    for reduce_s, readback_s, calls, lat in recs:
+        assert calls == 5 and reduce_s > 0 and readback_s >= 0 and lat > 0

@@ -326,6 +326,18 @@ def test_bench_spawns_ranks_on_the_gpu():
     for k in ("lane0_iters", "lane0_rel_l2_x", "lane_iters_min_max"):
         assert two["parity"][k] == one["parity"][k], k
     assert two["value"] > 0 and two["scaling"] == "weak"
+    # per-rank diagnostics: each rank's own elapsed time (the slowest one is the line's time, up to the closing
+    # barrier), lane-iterations summing to the job's, and the statistics all-reduce's host time
+    d = two["dist"]
+    el = d["rank_elapsed_s"]
+    assert len(el) == 2 and d["rank_elapsed_min_max"] == [min(el), max(el)]
+    total_s = two["ms_per_step"] * two["steps"] / 1e3
+    assert max(el) <= total_s + 1e-6 and max(el) > 0.9 * total_s, (el, total_s)
+    lanes = d["rank_lane_iterations"]
+    assert len(lanes) == 2 and abs(sum(lanes) - two["value"] * total_s) <= 1 and min(lanes) > 0
+    assert d["allreduce_calls_per_step"] > 0 and d["allreduce_8xf64_us"] > 0
+    assert all(0 <= t < total_s for t in d["rank_reduce_host_s"] + d["rank_readback_host_s"])
+    assert "rank_elapsed_s" not in one["dist"]
 
 
 def test_kernel_timing_covers_every_launch():

@@ -18,18 +18,32 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def code_object(lib, tmp):
+def code_objects(lib, tmp):
+    """The gfx950 code object of every translation unit (the .hip_fatbin section holds one offload bundle per
+    compiled source, concatenated)."""
     fb = os.path.join(tmp, os.path.basename(lib) + ".fatbin")
-    co = os.path.join(tmp, os.path.basename(lib) + ".co")
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fb], check=True)
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}", f"--output={co}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
-    return co
+    data = open(fb, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = []
+    i = data.find(magic)
+    while i >= 0:
+        starts.append(i)
+        i = data.find(magic, i + 1)
+    cos = []
+    for n, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
+        part = os.path.join(tmp, f"{os.path.basename(lib)}.{n}.bundle")
+        co = os.path.join(tmp, f"{os.path.basename(lib)}.{n}.co")
+        open(part, "wb").write(data[a:b])
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                        f"--output={co}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
+        cos.append(co)
+    return cos
 
 
-def kernels(co):
-    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", "--no-leading-addr", co],
-                         capture_output=True, text=True, check=True).stdout
+def kernels(cos):
+    out = "".join(subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", "--no-leading-addr", co],
+                                 capture_output=True, text=True, check=True).stdout for co in cos)
     ks, name = {}, None
     for line in out.splitlines():
         m = re.match(r"^([0-9a-f]+ )?<(.+)>:$", line.strip())
@@ -40,7 +54,7 @@ def kernels(co):
         if name is None:
             continue
         s = line.split("//")[0].strip()
-        if not s:
+        if not s or "file format" in s or s.startswith("Disassembly of section"):
             continue
         s = re.sub(r"<[^>]+>", "<L>", s)                  # branch targets by label
         s = re.sub(r"0x[0-9a-f]+", "IMM", s) if s.startswith("s_getpc") else s
@@ -55,7 +69,7 @@ def main():
     ap.add_argument("--show", default=None)
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
-        A, B = kernels(code_object(a.a, tmp)), kernels(code_object(a.b, tmp))
+        A, B = kernels(code_objects(a.a, tmp)), kernels(code_objects(a.b, tmp))
     only_a, only_b = sorted(set(A) - set(B)), sorted(set(B) - set(A))
     diff = sorted(k for k in set(A) & set(B) if A[k] != B[k])
     same = len(set(A) & set(B)) - len(diff)

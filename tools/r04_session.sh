@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 GPU session: named steps, each under its own time limit, chained so that the first failure (a test
+# failure, a fault, an abort, a time limit) ends the script.  Output under gpurun_out/r04/<name>.log.
+#   tools/r04_session.sh probe stress tests_carry bench ...
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+OUT=gpurun_out/r04
+mkdir -p $OUT
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a $OUT/steps.log
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] end $name rc=$rc" | tee -a $OUT/steps.log
+  tail -4 "$OUT/$name.log" | cut -c1-400
+  return $rc
+}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+  case $s in
+    probe) step mpc_rowbuf 150 python -u tools/mpc_rowbuf_probe.py --run || exit $? ;;
+    stress) step stress_parity 400 python -u tools/stress_parity.py full hard --out $OUT/stress || exit $? ;;
+    tests_carry) step pytest_carry 600 $PYT tests/test_gpu_parity.py -m gpu -k "carry or persistent_schedule or short_and_ragged" || exit $? ;;
+    tests_tail) step pytest_tail 600 $PYT tests/test_gpu_tail.py -m gpu || exit $? ;;
+    tests_bench) step pytest_bench 600 $PYT tests/test_gpu_workloads.py -m gpu -k "bench_spawns or cfg2" || exit $? ;;
+    tests_stress) step pytest_stress 600 $PYT tests/test_gpu_stress.py -m gpu || exit $? ;;
+    tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
+    smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) step bench 600 python -u bench.py || exit $? ;;
+    bench_cfg2) step bench_cfg2 300 python -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    bench_stress) step bench_stress 300 python -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    trace2) step trace_cfg2 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg2 -o run --output-format csv -- python3 -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    run2trace) step run2_trace 200 python -u tools/run2_trace.py build_ab/run2_trace.so || exit $? ;;
+    general) bash tools/r04_general_profile.sh || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

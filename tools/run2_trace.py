@@ -18,6 +18,7 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    os.environ["GYM_ALLOW_FOREIGN_BUILD"] = "1"     # a define-variant of this tree (its build id differs)
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--batch", type=int, default=4096)

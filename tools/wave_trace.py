@@ -31,6 +31,7 @@ def decode(hw, xcc):
 
 
 def main():
+    os.environ["GYM_ALLOW_FOREIGN_BUILD"] = "1"     # a define-variant of this tree (its build id differs)
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--batch", type=int, default=262144)
