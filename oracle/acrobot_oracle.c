@@ -196,7 +196,7 @@ double orc_forward(const orc_model* m, const orc_cost* c, const double* x, const
 }
 
 /* Optional per-iteration record of one lane (NULL pointers: not recorded).  Row k holds iteration k:
- * cost after the iteration (the reference's history['cost'][k+1]; the unchanged cost on an LS failure),
+ * cost after the iteration (the reference's history['cost'][k+1]; NaN for a failed one, which appends none),
  * max|sigma| of its sweep (history['sigma_norm'][k]), the Armijo trials it evaluated, and the tightest
  * Armijo test of the iteration: min over its trials of |J_new - (J + c gamma dJ)| / max(|J|, tiny) --
  * how far the closest accept / reject call was from a tie (a rounding-level value flags a decision that
@@ -238,7 +238,7 @@ static void solve_lane(const orc_model* m, const orc_cost* c, const double* x0, 
         }
         if (h && k < h->hist_len) {
             int64_t o = lane * h->hist_len + k;
-            if (h->cost) h->cost[o] = ok ? Jn : J;
+            if (h->cost) h->cost[o] = ok ? Jn : NAN;
             if (h->smax) h->smax[o] = smax;
             if (h->trials) h->trials[o] = ok ? i + 1 : max_ls;
             if (h->margin) h->margin[o] = tight;

@@ -71,7 +71,7 @@ def newton_solve(x0, x_ref, u_ref, max_iters=5000, tol=1e-4, beta=0.7, c=0.5, ga
     """Batched solve on host cores (OpenMP). x0 (B,4). Returns dict like acrobot_np.newton_solve.
 
     hist_len > 0 adds the per-iteration record of every lane, (B, hist_len) arrays, NaN / 0 past a lane's last
-    iteration: ``hist_cost`` (cost after iteration k; unchanged on an LS failure), ``hist_smax`` (max|sigma| of its
+    iteration: ``hist_cost`` (cost after iteration k; NaN for a failed iteration, as the GPU's history), ``hist_smax`` (max|sigma| of its
     sweep), ``hist_trials`` (Armijo trials evaluated) and ``hist_margin`` (the iteration's tightest Armijo test,
     min |J_new - (J + c gamma dJ)| / |J| over its trials: how close the closest accept / reject call was to a tie)."""
     x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)

@@ -187,3 +187,32 @@ def test_c_oracle_wide_start_lanes_match_reference(golden, task2_refs, max_iters
         a, b = o[k], W[m + k]
         e = np.linalg.norm((a - b).reshape(len(a), -1), axis=1) / np.linalg.norm(b.reshape(len(b), -1), axis=1)
         assert e.max() < spread[max_iters][k], (k, e.max())
+
+
+def test_c_oracle_stress_lanes_vs_reference(golden, task2_refs):
+    """The C oracle (with its per-iteration record) on the 27 stress lanes the reference itself was run on
+    (tests/golden/make_golden_stress.py: every lane whose status differs between the GPU and the oracle, 12 whose
+    counts differ, 6 LS-failure and 4 converged lanes on which they agree).  Until the first Armijo test within
+    1e-11 of a tie on either side the two cost histories agree to 1e-9 (the two take the same decisions); a lane
+    with no tie on either side has the reference's iteration count, status and rollout count exactly."""
+    g = golden("stress_ref_lanes")
+    x_ref, u_ref, _ = task2_refs
+    H = 5000
+    o = oc.newton_solve(g["x0"], x_ref, u_ref, max_iters=H, tol=1e-4, gamma_0=0.1, hist_len=H)
+    TIE = 1e-11
+    n_tie_free = 0
+    for j, lane in enumerate(g["lanes"]):
+        nr, no = int(g["n_iter"][j]), int(o["n_iter"][j])
+        mr, mo = g["margin"][j, :nr], o["hist_margin"][j, :no]
+        k_r = int(np.argmax(mr < TIE)) if (mr < TIE).any() else nr
+        k_o = int(np.argmax(mo < TIE)) if (mo < TIE).any() else no
+        k = min(k_r, k_o)
+        href, ho = g["cost"][j, 1:1 + k], o["hist_cost"][j, :k]       # NaN: a failed iteration (no cost after it)
+        assert np.array_equal(np.isnan(href), np.isnan(ho)), (int(lane), k)
+        fin = ~np.isnan(href)
+        assert np.all(np.abs(ho[fin] - href[fin]) <= 1e-9 * np.abs(href[fin])), (int(lane), k)
+        if k_r == nr and k_o == no:
+            n_tie_free += 1
+            assert (no, int(o["status"][j]), int(o["n_rollouts"][j])) == \
+                (nr, int(g["status"][j]), int(g["n_rollouts"][j])), int(lane)
+    assert n_tie_free >= 4          # the converged lanes
