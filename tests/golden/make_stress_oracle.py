@@ -41,7 +41,7 @@ def main():
     n_roll = np.zeros(LANES, np.int32)
     cost = np.zeros(LANES)
     k_tie = np.full(LANES, -1, np.int16)
-    margin_min = np.full(LANES, np.inf)
+    margin_min = np.full(LANES, np.inf, np.float32)
     t0 = time.time()
     for lo in range(0, LANES, a.chunk):
         hi = min(LANES, lo + a.chunk)
