@@ -32,6 +32,10 @@ for s in "$@"; do
     trace2) step trace_cfg2 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg2 -o run --output-format csv -- python3 -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
     run2trace) step run2_trace 200 python -u tools/run2_trace.py build_ab/run2_trace.so || exit $? ;;
     general) bash tools/r04_general_profile.sh || exit $? ;;
+    tailtrace) step tail_trace_base 200 python -u tools/tail_trace.py build_ab/tail_trace_base.so &&
+               step tail_trace_new 200 python -u tools/tail_trace.py build_ab/tail_trace_new.so || exit $? ;;
+    stress_ab) step stress_ab 600 env GYM_ALLOW_FOREIGN_BUILD=1 BENCH_ARGS="--workload stress --steps 2 --warmup 1 --no-cpu --extra-legs ''" \
+               bash tools/ab_alt_bench.sh r04/stress_ab 2 262144 build_ab/tail_base.so build_ab/tail_new.so || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
