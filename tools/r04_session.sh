@@ -30,6 +30,11 @@ for s in "$@"; do
     bench_cfg2) step bench_cfg2 300 python -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
     bench_stress) step bench_stress 300 python -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
     trace2) step trace_cfg2 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg2 -o run --output-format csv -- python3 -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    trace3) step trace_cfg3 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg3 -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    tracest) step trace_stress 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_stress -o run --output-format csv -- python3 -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    tracem) step trace_mpc 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_mpc -o run --output-format csv -- python3 -u bench.py --workload mpc --steps 20 --warmup 3 || exit $? ;;
+    fetch) step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_fetch -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
+    write) step pmc_write 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_write -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
     run2trace) step run2_trace 200 python -u tools/run2_trace.py build_ab/run2_trace.so || exit $? ;;
     general) bash tools/r04_general_profile.sh || exit $? ;;
     tailtrace) step tail_trace_base 200 python -u tools/tail_trace.py build_ab/tail_trace_base.so &&
