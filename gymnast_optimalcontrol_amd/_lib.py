@@ -23,7 +23,7 @@ EXPORTS = (
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
     "gym_riccati_general",
     "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase", "gym_newton_run",
-    "gym_newton_tail", "gym_newton_tail_scratch", "gym_newton_tail_lds",
+    "gym_newton_tail", "gym_newton_tail_scratch", "gym_newton_cand_scratch", "gym_newton_tail_lds",
     "gym_newton_finalize", "gym_newton_fill_states", "gym_newton_sigma",
     "gym_gamma_sweep", "gym_newton_gamma_sweep",
     "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_mpc_gains", "gym_lq_forward", "gym_track_rollout", "gym_track_rollout_ex",
@@ -32,7 +32,7 @@ EXPORTS = (
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run",
                 "tail")
 
-ABI_VERSION = 12        # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 13        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
@@ -76,7 +76,7 @@ class GymBatch(C.Structure):
                 ("cost", _P), ("dJ", _P), ("smax", _P), ("gamma", _P), ("status", _P), ("n_iter", _P),
                 ("res_buf", _P), ("n_roll", _P), ("retry_list", _P), ("counters", _P), ("cand_ok", _P),
                 ("partials", _P), ("stats", _P), ("hist_cost", _P), ("hist_smax", _P), ("lane_map", _P),
-                ("timing", C.POINTER(GymTiming))]
+                ("timing", C.POINTER(GymTiming)), ("cand_scratch", _P), ("cand_slots", C.c_int64)]
 
 
 _I64, _I32, _D = C.c_int64, C.c_int32, C.c_double
@@ -104,6 +104,7 @@ _SIGS = {
     "gym_newton_run": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_tail": [_MP, _WP, _AP, _BP, _P, _I32, _P, _I64, _I32, _I32, _P],
     "gym_newton_tail_scratch": [_I32, _I32, _I32, C.POINTER(C.c_int64)],
+    "gym_newton_cand_scratch": [_I32, _I64, C.POINTER(C.c_int64)],
     "gym_newton_tail_lds": [_I32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "gym_newton_finalize": [_MP, _WP, _BP, _I32, _P, _P, _P, _P, _P],
     "gym_newton_fill_states": [_MP, _BP, _I32, _P],

@@ -1483,7 +1483,114 @@ __global__ __launch_bounds__(BLK) void k_nt_candidates(Dyn m, KW w, SolverCtl a,
     }
 }
 
-// First accepted candidate per retry lane: re-run it writing the trajectory, update the lane.
+// Candidate scratch (gym_batch.cand_scratch, ABI 13): slot v holds candidate v's trajectory x (N, V/64, 2, 64) double2,
+// controls u (T, 2, V) planes and cost J (V); V = 0: no scratch (every accepted candidate is re-run).
+struct CandScratch {
+    double2* sx;
+    double* su;
+    double* sJ;
+    int64_t V;
+};
+
+// Armijo trials 2..max_ls on lane PAIRS: candidate i = r (max_ls - 1) + j - 1 (retry-list entry r, step gamma0 beta^j)
+// on lanes (2q, 2q + 1) of a wavefront, the offset-form feedback and gym::rk4_pair_fast -- the chain of
+// k_nt_candidates' single-lane rollout_cform<false, U0Z, true> with the joint-angle trigonometry split over the pair
+// (the same operations, the same bits).  Candidate i's trajectory, controls and cost also go to scratch slot i while
+// i < V, so that k_nt_retry copies the accepted one instead of re-running its chain.  The candidates of a launch
+// are few lanes' (most iterations of a hard solve have 0-30 lanes backtracking), so each launch is one chain long:
+// this halves the post-trial chains (candidates, then a copy instead of a second chain) and shortens the first.
+template <bool U0Z, bool RL = false>
+__global__ __launch_bounds__(BLK) void k_nt_cand_pair(Dyn m, KW w, SolverCtl a, TrialIO io,
+                                                      const double2* __restrict__ K1, const double* __restrict__ cs,
+                                                      const double* __restrict__ xr, const double* __restrict__ ur,
+                                                      const double* __restrict__ cost, const double* __restrict__ dJ,
+                                                      const int32_t* __restrict__ retry_list,
+                                                      const int32_t* __restrict__ counter,
+                                                      uint8_t* __restrict__ cand_ok, CandScratch sc, int64_t Bp, int N) {
+    const int nj = a.max_ls - 1;
+    const int64_t total = (int64_t)(*counter) * nj;
+    const int T = N - 1;
+    const bool odd = threadIdx.x & 1;
+    const uint32_t srow = (uint32_t)sc.V * 16u, splane = (uint32_t)sc.V * 8u;
+    const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
+    const char* Kb = reinterpret_cast<const char*>(K1);
+    const char* Cb = reinterpret_cast<const char*>(cs);
+    const char* Ub = reinterpret_cast<const char*>(io.u);
+    const char* Xs = reinterpret_cast<const char*>(sc.sx);
+    const char* Us = reinterpret_cast<const char*>(sc.su);
+    const gym::PolyRegs pk = gym::poly_vgprs_all();
+    Dyn dm = m;
+    gym::in_vgpr(dm.b); gym::in_vgpr(dm.d); gym::in_vgpr(dm.a2b); gym::in_vgpr(dm.bb); gym::in_vgpr(dm.dad);
+    gym::in_vgpr(dm.g1); gym::in_vgpr(dm.g2); gym::in_vgpr(dm.f1); gym::in_vgpr(dm.f2); gym::in_vgpr(dm.h);
+    gym::in_vgpr(dm.h2); gym::in_vgpr(dm.h6);
+    // wave-uniform trip count: every lane of the wavefront runs the pair step (DPP partners, its ballot)
+    for (int64_t base = (int64_t)blockIdx.x * (BLK / 2); base < total; base += (int64_t)gridDim.x * (BLK / 2)) {
+        const int64_t i0 = base + (threadIdx.x >> 1);
+        const bool act = i0 < total;
+        const int64_t i = act ? i0 : total - 1;          // a padding pair repeats the last candidate, unrecorded
+        const int64_t r = i / nj;
+        const int j = 1 + (int)(i % nj);
+        const int64_t l = retry_list[r];
+        double g = a.gamma0;
+        for (int q = 0; q < j; ++q) g *= a.beta;         // gamma_i *= beta, sequentially (:365)
+        const double dg = g - a.gamma0;
+        // this candidate's trajectory into slot i: the even lane stores (th1, th2) and the controls, the odd lane
+        // (w1, w2).  A store that must not land gets an offset past the buffer resource's range, which the
+        // hardware drops -- no branch around the stores, so the loop's wait counts stay exact (a store under a
+        // divergent branch would make the compiler wait for every store before the next stage's operands).
+        const bool keep = act && i < sc.V;
+        constexpr uint32_t OOB = 0x80000000u;            // > the resources' num_records (0x7fffffff)
+        const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+        const uint32_t v2 = keep ? wbo(i, 2) + (odd ? WROW : 0u) : OOB;
+        const uint32_t v1o = keep && !odd ? (uint32_t)i * 8u : OOB;
+        const double* xrl = lane_ref<RL>(xr, l, 4 * (int64_t)N);
+        const double* url = lane_ref<RL>(ur, l, 2 * (int64_t)T);
+        const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
+        double n0 = xa.x, n1 = xa.y, n2 = xb.x, n3 = xb.y;
+        bst2(rsrc(Xs), v2, 0, odd ? n2 : n0, odd ? n3 : n1);
+        auto fetch = [&](TrialStage& q, int t) {
+            const auto rK = rsrc(Kb + (int64_t)t * (2 * (int64_t)row));
+            q.k0 = bld2(rK, o2, 0);
+            q.k1 = bld2(rK, o2, WROW);
+            const auto rC = rsrc(Cb + (int64_t)t * row);
+            q.cg = bld1(rC, o1, 0);
+            q.s1 = bld1(rC, o1, plane);
+            q.u0 = U0Z ? 0.0 : bld1(rsrc(Ub + (int64_t)t * row), o1, 0);
+        };
+        const double G00 = w.G00, iG00 = w.iG00;
+        double J = 0.0;
+        TrialStage pre;
+        fetch(pre, 0);
+        for (int t = 0; t < T; ++t) {
+            const TrialStage q = pre;
+            if (t + 1 < T) fetch(pre, t + 1);
+            const double* urt = url + 2 * t;
+            const double v0 = U0Z ? 0.0 : trial_u0(q.u0, urt[0], g, G00, iG00);   // U0Z: +0 exactly
+            const double v1 = trial_u1_sig(q.k0, q.k1, q.cg, q.s1, dg, n0, n1, n2, n3);
+            const double f0 = U0Z ? 0.0 : v0 - urt[0], f1 = v1 - urt[1];
+            J = stage_cost<U0Z>(J, w.Q, w.R, n0, n1, n2, n3, xrl + 4 * t, f0, f1);
+            {
+                const auto rO = rsrc(Us + (int64_t)t * srow);
+                if (!U0Z) bst1(rO, v1o, 0, v0);
+                bst1(rO, v1o, splane, v1);
+            }
+            gym::rk4_pair_fast<true>(dm, odd, n0, n1, n2, n3, v1, pk);
+            bst2(rsrc(Xs + (int64_t)(t + 1) * (2 * (int64_t)srow)), v2, 0, odd ? n2 : n0, odd ? n3 : n1);
+        }
+        const double Jn = J + xcost(w.QT, n0, n1, n2, n3, xrl + 4 * T);
+        if (act && !odd) {
+            cand_ok[(int64_t)j * Bp + l] = (Jn < cost[l] + a.c * g * dJ[l]) ? 1 : 0;
+            if (keep) sc.sJ[i] = Jn;
+        }
+    }
+}
+
+// First accepted candidate per retry lane: its trajectory into the lane's next iterate (io.xn / io.un), the lane
+// updated.  Work item (r, c): retry-list entry r and knot chunk c (CPK knots); with a scratch slot the items copy
+// the candidate's knots from it (k_nt_cand_pair) and item (r, 0) books the lane with the candidate's recorded cost;
+// without one (V = 0, or a slot index past V) item (r, 0) re-runs the candidate writing the trajectory (its
+// rollout_cform: the same bits as the copy).
+constexpr int CPK = 8;   // knots per copy item
 template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                   const double2* __restrict__ K1, const double* __restrict__ cs,
@@ -1494,14 +1601,42 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
                                                   int32_t* __restrict__ n_roll, const int32_t* __restrict__ retry_list,
                                                   const int32_t* __restrict__ counter,
                                                   const uint8_t* __restrict__ cand_ok, double* __restrict__ hist_cost,
-                                                  int64_t Bp, int N) {
+                                                  CandScratch sc, int64_t Bp, int N) {
     const int nr = *counter;
     const int nj = a.max_ls - 1;
-    for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < nr; i += (int64_t)gridDim.x * BLK) {
-        const int64_t l = retry_list[i];
-        int jacc = 0;
-        for (int j = 1; j <= nj; ++j)
-            if (cand_ok[(int64_t)j * Bp + l]) { jacc = j; break; }
+    const int T = N - 1;
+    const int nc = sc.V > 0 ? (N + CPK - 1) / CPK : 1;   // items per retry lane
+    const int64_t total = (int64_t)nr * nc;
+    for (int64_t it = (int64_t)blockIdx.x * BLK + threadIdx.x; it < total; it += (int64_t)gridDim.x * BLK) {
+        const int64_t ri = it / nc;
+        const int c = (int)(it % nc);
+        const int64_t l = retry_list[ri];
+        int jacc = 0;                                    // the first accepted candidate (0: none)
+        for (int j0 = 1; j0 <= nj && jacc == 0; j0 += 8) {   // eight independent byte loads per round
+            uint8_t ok[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ok[q] = j0 + q <= nj ? cand_ok[(int64_t)(j0 + q) * Bp + l] : 0;
+#pragma unroll
+            for (int q = 7; q >= 0; --q)
+                if (ok[q]) jacc = j0 + q;
+        }
+        const int64_t v = ri * nj + jacc - 1;
+        const bool copy = jacc > 0 && v < sc.V;
+        if (copy) {
+#pragma unroll
+            for (int q = 0; q < CPK; ++q) {
+                const int t = c * CPK + q;
+                if (t < N) {
+                    io.xn[wix(t, 0, 2, l, Bp)] = sc.sx[wix(t, 0, 2, v, sc.V)];
+                    io.xn[wix(t, 1, 2, l, Bp)] = sc.sx[wix(t, 1, 2, v, sc.V)];
+                }
+                if (t < T) {
+                    if (!U0Z) io.un[pix(t, 0, 2, l, Bp)] = sc.su[pix(t, 0, 2, v, sc.V)];
+                    io.un[pix(t, 1, 2, l, Bp)] = sc.su[pix(t, 1, 2, v, sc.V)];
+                }
+            }
+        }
+        if (c != 0) continue;
         n_iter[l] += 1;
         if (jacc == 0) {
             n_roll[l] += nj;
@@ -1511,10 +1646,15 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
         n_roll[l] += jacc;
         double g = a.gamma0;
         for (int q = 0; q < jacc; ++q) g *= a.beta;
-        const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
-        const double Jn = rollout_cform<true, U0Z, true, CK>(m, w, io.u, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N),
-                                                             lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), io.xn, io.un, g,
-                                                             a.gamma0, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+        double Jn;
+        if (copy) {
+            Jn = sc.sJ[v];
+        } else {
+            const double2 xa = io.x[wix(0, 0, 2, l, Bp)], xb = io.x[wix(0, 1, 2, l, Bp)];
+            Jn = rollout_cform<true, U0Z, true, CK>(m, w, io.u, K1, cs, lane_ref<RL>(xr, l, 4 * (int64_t)N),
+                                                    lane_ref<RL>(ur, l, 2 * (int64_t)(N - 1)), io.xn, io.un, g,
+                                                    a.gamma0, l, Bp, N, xa.x, xa.y, xb.x, xb.y);
+        }
         accept_lane(a, l, Jn, g, smax[l], cost, gamma, status, res_buf, hist_cost, Bp);
     }
 }
@@ -3064,7 +3204,8 @@ int gym_riccati_general(const double* A, const double* Bm, const double* Q, cons
 // every batch entry point: the buffers, the sizes and the flag combination (per-lane references are never
 // combined with state checkpointing: no kernel instantiates both)
 static bool bad_batch(const gym_batch* b) {
-    return !b || bad_dims(b->B, b->Bp, b->N) || !b->x[0] || !b->x[1] || !b->u[0] || !b->u[1] || !b->K1 || !b->cs ||
+    return !b || bad_dims(b->B, b->Bp, b->N) || (b->cand_scratch && (b->cand_slots < 0 || b->cand_slots % BLK != 0 ||
+                                                                    b->cand_slots > GYM_MAX_BP)) || !b->x[0] || !b->x[1] || !b->u[0] || !b->u[1] || !b->K1 || !b->cs ||
            !b->x_ref || !b->u_ref || !b->cost || !b->dJ || !b->smax || !b->gamma || !b->status || !b->n_iter ||
            !b->res_buf || !b->n_roll || !b->retry_list || !b->counters || !b->partials || !b->stats ||
            ((b->flags & GYM_FLAG_REF_LANE) && (b->flags & GYM_FLAG_X_CKPT));
@@ -3097,6 +3238,18 @@ int gym_newton_init(const gym_model* m, const gym_weights* w, const double* x0, 
 // launch latency, not workgroup dispatch.
 constexpr int64_t POST_CAP = 2048;
 constexpr int64_t CAND_CAP = 4096;
+// the candidate scratch of the batch (gym_batch.cand_scratch): none without lane-pair candidates or with state
+// checkpointing (whose accepted re-run stores the checkpoint knots only)
+static CandScratch cand_scratch(const gym_batch* b, bool pair) {
+    CandScratch c{nullptr, nullptr, nullptr, 0};
+    if (!pair || !b->cand_scratch || b->cand_slots <= 0 || (b->flags & GYM_FLAG_X_CKPT)) return c;
+    const int64_t V = b->cand_slots, N = b->N;
+    c.sx = (double2*)b->cand_scratch;
+    c.su = b->cand_scratch + 4 * N * V;
+    c.sJ = c.su + 2 * (N - 1) * V;
+    c.V = V;
+    return c;
+}
 static void launch_post_trial(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* b,
                               const SolverCtl& c, const TrialIO& io, Range rg, int32_t* counter, double* stats_out,
                               const double* other, double* total, hipStream_t st, bool sigma_streamed = false) {
@@ -3111,16 +3264,26 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
                                kw(*w), io.x, io.u, b->x_ref, b->u_ref, b->cs, b->retry_list + rg.lo, counter,
                                (const int32_t*)nullptr, -1, b->B, b->Bp, b->N);
         }
+        // candidates on lane pairs (recorded in the scratch slots, if any) unless single-lane chains were asked for
+        const bool pair = !(b->flags & GYM_FLAG_RUN_SINGLE);
+        const CandScratch sc = cand_scratch(b, pair);
+        const int64_t ncand = n * (int64_t)(a->max_ls - 1);
         {
             TimedLaunch tl(b->timing, 2, st);
-            const int gc = grid_for(n * (int64_t)(a->max_ls - 1), BLK, CAND_CAP);
-            hipLaunchKernelGGL(CAND_SEL(b, k_nt_candidates), dim3(gc), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref,
-                               b->cost, b->dJ, b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
+            if (pair)
+                hipLaunchKernelGGL(CAND_SEL(b, k_nt_cand_pair), dim3(grid_for(2 * ncand, BLK, CAND_CAP)), dim3(BLK), 0,
+                                   st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref, b->cost, b->dJ,
+                                   b->retry_list + rg.lo, counter, b->cand_ok, sc, b->Bp, b->N);
+            else
+                hipLaunchKernelGGL(CAND_SEL(b, k_nt_candidates), dim3(grid_for(ncand, BLK, CAND_CAP)), dim3(BLK), 0,
+                                   st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref, b->cost, b->dJ,
+                                   b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
+        const int64_t items = sc.V > 0 ? n * ((b->N + CPK - 1) / CPK) : n;
         TimedLaunch tl(b->timing, 3, st);
-        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(n, BLK, POST_CAP)), dim3(BLK), 0, st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref,
-                           b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter, b->res_buf, b->n_roll,
-                           b->retry_list + rg.lo, counter, b->cand_ok, hc, b->Bp, b->N);
+        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(items, BLK, POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
+                           kw(*w), c, io, K1, cs, b->x_ref, b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter,
+                           b->res_buf, b->n_roll, b->retry_list + rg.lo, counter, b->cand_ok, hc, sc, b->Bp, b->N);
     }
     TimedLaunch tl(b->timing, 4, st);
     hipLaunchKernelGGL(k_stats_partial, dim3(STAT_BLOCKS), dim3(STAT_THREADS), 0, st, b->status, b->cost, b->smax,
@@ -3276,6 +3439,12 @@ int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t*
     const int64_t v = (int64_t)n_lanes * max_ls;
     const int64_t Vp = v > 0 ? (v + BLK - 1) / BLK * BLK : BLK;
     *doubles_out = Vp * (4 * (int64_t)N + 2 * (int64_t)(N - 1));
+    return 0;
+}
+
+int gym_newton_cand_scratch(int32_t N, int64_t slots, int64_t* doubles_out) {
+    if (!doubles_out || N < 2 || slots < 0 || slots % BLK != 0 || slots > GYM_MAX_BP) return GYM_EINVAL;
+    *doubles_out = slots * (4 * (int64_t)N + 2 * (int64_t)(N - 1) + 1);
     return 0;
 }
 

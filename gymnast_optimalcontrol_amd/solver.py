@@ -84,6 +84,9 @@ class BatchedNewtonSolver:
     # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
     # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.
     TAIL_LANES_PER_CU = 4
+    # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
+    # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
+    CAND_SLOTS = 32768
 
     @staticmethod
     def pipeline_min_lanes(device) -> int:
@@ -101,7 +104,7 @@ class BatchedNewtonSolver:
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
                  capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
                  capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128,
-                 compact: bool | None = None, world_size: int = 1):
+                 compact: bool | None = None, world_size: int = 1, cand_slots: int | None = None):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -243,6 +246,22 @@ class BatchedNewtonSolver:
         self.serial_switch_at = None   # the iteration the low-occupancy switch happened at
         self._its_switch, self._its_tail_start = 0, None
         self._tail_scratch = None
+        # candidate scratch (gym_batch.cand_scratch, ABI 13): the post-trial Armijo candidates of the serial /
+        # pipelined schedules and the low-occupancy regime record their trajectories, and the accepted one is copied
+        # instead of re-run (a T-step chain per backtracking iteration).  Slots for min(lanes x (max_ls - 1),
+        # cand_slots) candidates (~24 KiB each at T = 500); lanes past them are re-run.  The straggler tail borrows
+        # the same buffer.  0 turns it off (the same bits either way).
+        if cand_slots is None:
+            cand_slots = self.CAND_SLOTS
+        slots = min(self.Bp * max(int(max_ls) - 1, 0), int(cand_slots))
+        slots = slots // 64 * 64
+        self._cand_scratch = None
+        if (slots > 0 and not self.persistent and not self.checkpoint and self.split_waves):
+            need = C.c_int64()
+            _lib.check(engine.lib.gym_newton_cand_scratch(self.N, slots, C.byref(need)), "gym_newton_cand_scratch")
+            self._cand_scratch = torch.empty(int(need.value), dtype=F64, device=dev)
+            b.cand_scratch, b.cand_slots = self._cand_scratch.data_ptr(), slots
+        self.cand_slots = slots if self._cand_scratch is not None else 0
         self.tail_lane_its = 0
         self._cap_pos = None
         self._cap_log = []
@@ -326,10 +345,13 @@ class BatchedNewtonSolver:
         need = C.c_int64()
         _lib.check(self.eng.lib.gym_newton_tail_scratch(self.N, n, int(self.armijo.max_ls), C.byref(need)),
                    "gym_newton_tail_scratch")
-        if self._tail_scratch is None or self._tail_scratch.numel() < need.value:
-            self._tail_scratch = None
-            self._tail_scratch = torch.empty(int(need.value), dtype=F64, device=self.eng.device)
-        sc = self._tail_scratch
+        if self._cand_scratch is not None and self._cand_scratch.numel() >= need.value:
+            sc = self._cand_scratch          # the candidate scratch (the tail and the post-trial kernels never overlap)
+        else:
+            if self._tail_scratch is None or self._tail_scratch.numel() < need.value:
+                self._tail_scratch = None
+                self._tail_scratch = torch.empty(int(need.value), dtype=F64, device=self.eng.device)
+            sc = self._tail_scratch
         self.launches["tail"] += 1
         _lib.check(self.eng.lib.gym_newton_tail(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.armijo),
                                                 C.byref(self.batch), lanes.data_ptr() if n else None, n,

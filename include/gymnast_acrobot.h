@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 12
+#define GYM_ABI_VERSION 13
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -153,6 +153,16 @@ typedef struct gym_batch {
     const int64_t* lane_map; /* optional (B): lane i's results go to row lane_map[i] of the lane-major outputs
                          * of gym_newton_finalize / gym_newton_sigma (a permutation; NULL: identity)  */
     gym_timing* timing; /* [host] optional kernel timing (NULL: none)               */
+    /* optional (ABI 13) candidate scratch of the post-trial Armijo search (gym_newton_iteration / _phase / _run with
+     * GYM_FLAG_SIGMA_STREAM): candidate i = r (max_ls - 1) + j - 1 (retry-list entry r, step gamma0 beta^j) stores
+     * its trajectory, controls and cost in slot i while i < cand_slots, and the accepted one is then copied into
+     * the lane's next iterate instead of re-running its rollout (a chain of T RK4 steps); candidates without a
+     * slot are re-run as before.  cand_scratch: gym_newton_cand_scratch(N, cand_slots) doubles, laid out as
+     * x (N, V/64, 2, 64) double2 | u (T, 2, V) planes | J (V), V = cand_slots (a multiple of 64).
+     * cand_slots = 0 (or NULL): every accepted candidate is re-run.  Not used with GYM_FLAG_X_CKPT or
+     * GYM_FLAG_RUN_SINGLE (their candidates keep the single-lane re-run path).  Bits are the same either way. */
+    double* cand_scratch;
+    int64_t cand_slots;
 } gym_batch;
 
 int gym_abi_version(void);
@@ -262,6 +272,8 @@ int gym_newton_tail(const gym_model* m, const gym_weights* w, const gym_armijo* 
                     int32_t k1, void* stream);
 /* [host] Scratch doubles gym_newton_tail needs for n_lanes lanes (candidate trajectories of every trial). */
 int gym_newton_tail_scratch(int32_t N, int32_t n_lanes, int32_t max_ls, int64_t* doubles_out);
+/* [host] Doubles of gym_batch.cand_scratch for `slots` candidate slots (a multiple of 64, >= 0) at horizon N. */
+int gym_newton_cand_scratch(int32_t N, int64_t slots, int64_t* doubles_out);
 /* LDS per workgroup the tail kernel needs at horizon N (*bytes_out; ~72 KiB at N = 501), and, if limit_out is not
  * NULL, the current device's opt-in limit (hipDeviceAttributeSharedMemPerBlockOptin; a HIP error code if the
  * device cannot be queried).  A caller turns the tail off up front when bytes > limit (solver.py tail_ok). */

@@ -133,8 +133,8 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
     D = 0x10000
     m, w, a = _lib.GymModel(dt=0.02), _lib.GymWeights(), _lib.GymArmijo(1e-4, 0.7, 0.5, 0.1, 20, 0)
 
-    def batch(B=64, Bp=64, N=501, flags=0):
-        b = _lib.GymBatch(B=B, Bp=Bp, N=N, flags=flags)
+    def batch(B=64, Bp=64, N=501, flags=0, cand_slots=0):
+        b = _lib.GymBatch(B=B, Bp=Bp, N=N, flags=flags, cand_slots=cand_slots)
         for f, t in _lib.GymBatch._fields_:
             if f in ("x", "u"):
                 getattr(b, f)[0] = getattr(b, f)[1] = D
@@ -144,7 +144,7 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
 
     R = C.byref
     for b in (batch(B=0), batch(B=65, Bp=64), batch(B=60, Bp=100), batch(N=1), batch(Bp=_lib.MAX_BP + 64),
-              batch(flags=_lib.FLAG_REF_LANE | _lib.FLAG_X_CKPT)):
+              batch(flags=_lib.FLAG_REF_LANE | _lib.FLAG_X_CKPT), batch(cand_slots=100), batch(cand_slots=-64)):
         rcs = [lib.gym_newton_init(R(m), R(w), D, R(b), None),
                lib.gym_newton_iteration(R(m), R(w), R(a), R(b), 0, None),
                lib.gym_newton_phase(R(m), R(w), R(a), R(b), 0, 1, None),
@@ -160,6 +160,11 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
     need = C.c_int64()
     assert lib.gym_newton_tail_scratch(501, 3, 20, C.byref(need)) == 0 and need.value == 64 * (4 * 501 + 2 * 500)
     assert lib.gym_newton_tail_scratch(501, 3, 65, C.byref(need)) == 1                  # > 64 trials
+    # candidate scratch (ABI 13): x pairs, u planes and a cost per slot; slots a multiple of 64
+    assert lib.gym_newton_cand_scratch(501, 128, C.byref(need)) == 0 and need.value == 128 * (4 * 501 + 2 * 500 + 1)
+    assert lib.gym_newton_cand_scratch(501, 0, C.byref(need)) == 0 and need.value == 0
+    assert lib.gym_newton_cand_scratch(501, 100, C.byref(need)) == 1
+    assert lib.gym_newton_cand_scratch(1, 64, C.byref(need)) == 1
     # the tail's LDS at T = 500: above the 64 KiB default, within gfx950's 160 KiB (the device limit is queried
     # only when asked for, so this runs without a device); horizons past the staging are refused
     lds = C.c_int64()

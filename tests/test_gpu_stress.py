@@ -146,6 +146,70 @@ def test_stress_hard_lanes_vs_live_oracle():
     assert np.max(np.abs(cg[conv] - o["cost"][conv]) / np.abs(o["cost"][conv])) < 1e-11
 
 
+def _oracle_groups(x0, xr, ur, H):
+    """The C oracle (shared references only) over per-lane references: one run per distinct reference, merged."""
+    from oracle import c_oracle
+    if xr.ndim == 2:
+        return c_oracle.newton_solve(x0, xr, ur, max_iters=H, tol=1e-4, gamma_0=0.1, hist_len=H)
+    keys = [ur[l].tobytes() + xr[l].tobytes() for l in range(len(x0))]
+    out = None
+    for key in dict.fromkeys(keys):
+        idx = np.array([l for l, k in enumerate(keys) if k == key])
+        o = c_oracle.newton_solve(x0[idx], xr[idx[0]], ur[idx[0]], max_iters=H, tol=1e-4, gamma_0=0.1, hist_len=H)
+        if out is None:
+            out = {k: np.empty((len(x0),) + v.shape[1:], v.dtype) for k, v in o.items()}
+        for k, v in o.items():
+            out[k][idx] = v
+    return out
+
+
+@pytest.mark.parametrize("kind", ["task1", "per_lane"])
+def test_stress_general_paths_vs_live_oracle(kind):
+    """The same contract on the paths the headline does not take: task 1's live tau1 channel (the general,
+    tau1-streaming kernels; tests/golden task1_solve's references) and per-lane references (every third lane's
+    u_ref scaled by 0.8; the oracle runs each distinct reference separately), 2,048 hard lanes through the automatic
+    schedule of a 262,144-lane shard with the tail at 128 lanes."""
+    from gymnast_optimalcontrol_amd import _lib
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    x0 = _hard_x0()
+    B, H = len(x0), 5000
+    if kind == "task1":
+        g = load_golden("task1_solve")
+        xr, ur = g["x_ref"], g["u_ref_full"]
+        assert np.abs(ur[:, 0]).max() > 0                                   # the live tau1 channel
+    else:
+        from bench import load_refs
+        xr, ur = load_refs()
+        xr = np.broadcast_to(xr, (B,) + xr.shape).copy()
+        ur = np.broadcast_to(ur, (B,) + ur.shape).copy()
+        ur[1::3, :, 1] *= 0.8
+    s = BatchedNewtonSolver(AcrobotEngine(), xr, ur, B, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20,
+                            hist_len=H, schedule_lanes=262144, tail_lanes=128)
+    r = s.solve(x0, H, sync_every=4)
+    assert r.schedule == "pipelined" and r.tail_lane_iterations > 0
+    o = _oracle_groups(x0, xr, ur, H)
+    ng, sg, rg = _decisions(r)
+    same = (ng == o["n_iter"]) & (sg == o["status"]) & (rg == o["n_rollouts"])
+    hg = r.hist_cost.cpu().numpy().T
+    for l in np.nonzero(~same)[0]:
+        k = _first_divergence(hg[l], o["hist_cost"][l], int(ng[l]), int(o["n_iter"][l]))
+        assert np.nanmin(o["hist_margin"][l, :k + 1]) < TIE, (int(l), k)
+    tie_free = ~(np.nanmin(np.where(np.isnan(o["hist_margin"]), np.inf, o["hist_margin"]), axis=1) < TIE)
+    assert tie_free.sum() > B // 4 and same[tie_free].all()
+    conv = same & (o["status"] == _lib.CONVERGED)
+    assert conv.sum() > 20 and (o["status"] == _lib.LS_FAILED).sum() > 50
+    xg = r.x.cpu().numpy()[conv]
+    ex = np.linalg.norm((xg - o["x"][conv]).reshape(conv.sum(), -1), axis=1) / \
+        np.linalg.norm(o["x"][conv].reshape(conv.sum(), -1), axis=1)
+    assert ex.max() < 1e-8, ex.max()
+    cg = r.cost.cpu().numpy()
+    assert np.max(np.abs(cg[conv] - o["cost"][conv]) / np.abs(o["cost"][conv])) < 1e-11
+    print(kind, "regimes: compactions", r.compactions, "lowocc", r.lowocc_lane_iterations, "tail",
+          r.tail_lane_iterations, "same", int(same.sum()), "tie-free", int(tie_free.sum()),
+          "statuses", np.bincount(o["status"]))
+
+
 def test_stress_lanes_vs_reference():
     """The reference's own newton_Algorithm on 27 stress lanes (tests/golden/stress_ref_lanes.npz: every lane whose
     status differs between the GPU and the oracle, 12 lanes whose counts differ, 6 LS-failure and 4 converged lanes

@@ -124,6 +124,40 @@ def test_straggler_tail_on_short_and_ragged_horizons(N):
         _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"N={N}: {f}")
 
 
+@pytest.mark.parametrize("kind", ["serial", "pipelined", "task1", "per_lane"])
+def test_candidate_scratch_is_invisible(kind):
+    """The post-trial Armijo search with its candidate scratch (ABI 13: lane-pair candidates recording their
+    trajectories, the accepted one copied) against the same solve re-running every accepted candidate
+    (cand_slots=0), with too few slots for the backtracking lanes (128: most re-run, some copied), and with
+    single-lane candidates (split_waves=False, k_nt_candidates): every output bit for bit, over the serial and
+    pipelined schedules, the live tau1 channel and per-lane references, lane compaction and the low-occupancy
+    regime included (the tail off, so that every backtracking iteration goes through the post-trial kernels)."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    B, max_iters = 1000, 300
+    x0 = _hard_lanes(B, seed=13)
+    if kind == "per_lane":
+        xr, ur = _refs("task2")
+        xr = np.broadcast_to(xr, (B,) + xr.shape).copy()
+        ur = np.broadcast_to(ur, (B,) + ur.shape).copy()
+        ur[1::3, :, 1] *= 0.8
+    else:
+        xr, ur = _refs("task1" if kind == "task1" else "task2")
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, hist_len=max_iters, tail_lanes=0,
+              pipeline=kind == "pipelined", compact=kind != "task1")
+    r = BatchedNewtonSolver(eng, xr, ur, B, cand_slots=0, **kw).solve(x0, max_iters, sync_every=3)
+    assert int((r.n_rollouts > r.n_iter).sum()) > 100          # backtracking lanes
+    for name, skw in {"default slots": {}, "128 slots": dict(cand_slots=128),
+                      "single-lane candidates": dict(split_waves=False)}.items():
+        s = BatchedNewtonSolver(eng, xr, ur, B, **skw, **kw)
+        assert s.cand_slots == {"default slots": min(s.Bp * 19, s.CAND_SLOTS), "128 slots": 128,
+                                "single-lane candidates": 0}[name]
+        t = s.solve(x0, max_iters, sync_every=3)
+        for f in FIELDS:
+            _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{kind} / {name}: {f}")
+
+
 @pytest.mark.parametrize("kind", ["pipelined", "serial", "per_lane_noreorder", "serial_single_wave"])
 def test_lane_compaction_is_invisible(kind):
     """The low-occupancy switch forced at every host synchronisation (compact="force"): lane compaction

@@ -24,6 +24,8 @@ for s in "$@"; do
     tests_tail) step pytest_tail 600 $PYT tests/test_gpu_tail.py -m gpu || exit $? ;;
     tests_bench) step pytest_bench 600 $PYT tests/test_gpu_workloads.py -m gpu -k "bench_spawns or cfg2" || exit $? ;;
     tests_stress) step pytest_stress 600 $PYT tests/test_gpu_stress.py -m gpu || exit $? ;;
+    tests_cand) step pytest_cand 600 $PYT tests/test_gpu_tail.py -m gpu -k "candidate_scratch" || exit $? ;;
+    cand_ab) step cand_ab 400 python -u tools/cand_ab.py --rounds 3 || exit $? ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
