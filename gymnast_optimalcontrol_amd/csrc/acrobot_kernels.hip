@@ -1498,7 +1498,10 @@ struct CandScratch {
 // (the same operations, the same bits).  Candidate i's trajectory, controls and cost also go to scratch slot i while
 // i < V, so that k_nt_retry copies the accepted one instead of re-running its chain.  The candidates of a launch
 // are few lanes' (most iterations of a hard solve have 0-30 lanes backtracking), so each launch is one chain long:
-// this halves the post-trial chains (candidates, then a copy instead of a second chain) and shortens the first.
+// this halves the post-trial chains (candidates, then a copy instead of a second chain).  Stress workload, same
+// process (tools/cand_ab.py, profiles/r04/cand/): +6.3% against re-running the accepted candidate; the candidates
+// launch 42.5 ms per 193 sampled launches on pairs with the stores, 47.5 on single lanes with the stores, 39.1 for the
+// former single-lane cost-only chain.
 template <bool U0Z, bool RL = false>
 __global__ __launch_bounds__(BLK) void k_nt_cand_pair(Dyn m, KW w, SolverCtl a, TrialIO io,
                                                       const double2* __restrict__ K1, const double* __restrict__ cs,

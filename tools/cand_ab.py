@@ -52,10 +52,10 @@ def main():
                   f"{kt['retry'][1]}  tail {kt['tail'][0]:.1f} ms  (sampled post-trial pairs)", flush=True)
             res[name] = {f: getattr(r, f).cpu() for f in ("n_iter", "status", "n_rollouts", "cost", "x")}
             del r
-    same = all(torch.equal(res["rerun"][f], res["scratch"][f]) for f in res["rerun"])
+    same = all(torch.equal(res["rerun"][f], res[k][f]) for k in res for f in res["rerun"])
     med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
-    print(f"median s/solve: rerun {med['rerun']:.3f}, scratch {med['scratch']:.3f} "
-          f"({med['rerun'] / med['scratch'] - 1:+.2%} throughput); outcomes bitwise equal: {same}", flush=True)
+    print("median s/solve: " + ", ".join(f"{k} {v:.3f} ({med['rerun'] / v - 1:+.2%})" for k, v in med.items()) +
+          f"; outcomes bitwise equal: {same}", flush=True)
     if not same:
         sys.exit(1)
 
