@@ -1589,10 +1589,12 @@ __global__ __launch_bounds__(BLK) void k_nt_cand_pair(Dyn m, KW w, SolverCtl a, 
 }
 
 // First accepted candidate per retry lane: its trajectory into the lane's next iterate (io.xn / io.un), the lane
-// updated.  Work item (r, c): retry-list entry r and knot chunk c (CPK knots); with a scratch slot the items copy
-// the candidate's knots from it (k_nt_cand_pair) and item (r, 0) books the lane with the candidate's recorded cost;
-// without one (V = 0, or a slot index past V) item (r, 0) re-runs the candidate writing the trajectory (its
-// rollout_cform: the same bits as the copy).
+// updated.  Work items: first one head item per retry-list entry r (its bookkeeping; without a scratch slot for its
+// accepted candidate -- V = 0, or a slot index past V -- the re-run of that candidate writing the trajectory, its
+// rollout_cform: the same bits as the copy), then, with scratch, one copy item per entry and knot chunk (CPK knots).
+// Head items on consecutive threads: the re-runs of a launch with more backtracking lanes than slots run side by
+// side, one chain each (with the copy items interleaved, a thread could draw several: stress trace, launches of
+// up to 2.2 ms).
 constexpr int CPK = 8;   // knots per copy item
 template <bool U0Z, bool CK, bool RL = false>
 __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, TrialIO io,
@@ -1608,11 +1610,12 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
     const int nr = *counter;
     const int nj = a.max_ls - 1;
     const int T = N - 1;
-    const int nc = sc.V > 0 ? (N + CPK - 1) / CPK : 1;   // items per retry lane
-    const int64_t total = (int64_t)nr * nc;
+    const int nc = sc.V > 0 ? (N + CPK - 1) / CPK : 0;   // copy items per retry lane
+    const int64_t total = (int64_t)nr * (1 + nc);
     for (int64_t it = (int64_t)blockIdx.x * BLK + threadIdx.x; it < total; it += (int64_t)gridDim.x * BLK) {
-        const int64_t ri = it / nc;
-        const int c = (int)(it % nc);
+        const bool head = it < nr;
+        const int64_t ri = head ? it : (it - nr) / nc;
+        const int c = head ? 0 : (int)((it - nr) % nc);
         const int64_t l = retry_list[ri];
         int jacc = 0;                                    // the first accepted candidate (0: none)
         for (int j0 = 1; j0 <= nj && jacc == 0; j0 += 8) {   // eight independent byte loads per round
@@ -1625,21 +1628,23 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
         }
         const int64_t v = ri * nj + jacc - 1;
         const bool copy = jacc > 0 && v < sc.V;
-        if (copy) {
+        if (!head) {
+            if (copy) {
 #pragma unroll
-            for (int q = 0; q < CPK; ++q) {
-                const int t = c * CPK + q;
-                if (t < N) {
-                    io.xn[wix(t, 0, 2, l, Bp)] = sc.sx[wix(t, 0, 2, v, sc.V)];
-                    io.xn[wix(t, 1, 2, l, Bp)] = sc.sx[wix(t, 1, 2, v, sc.V)];
-                }
-                if (t < T) {
-                    if (!U0Z) io.un[pix(t, 0, 2, l, Bp)] = sc.su[pix(t, 0, 2, v, sc.V)];
-                    io.un[pix(t, 1, 2, l, Bp)] = sc.su[pix(t, 1, 2, v, sc.V)];
+                for (int q = 0; q < CPK; ++q) {
+                    const int t = c * CPK + q;
+                    if (t < N) {
+                        io.xn[wix(t, 0, 2, l, Bp)] = sc.sx[wix(t, 0, 2, v, sc.V)];
+                        io.xn[wix(t, 1, 2, l, Bp)] = sc.sx[wix(t, 1, 2, v, sc.V)];
+                    }
+                    if (t < T) {
+                        if (!U0Z) io.un[pix(t, 0, 2, l, Bp)] = sc.su[pix(t, 0, 2, v, sc.V)];
+                        io.un[pix(t, 1, 2, l, Bp)] = sc.su[pix(t, 1, 2, v, sc.V)];
+                    }
                 }
             }
+            continue;
         }
-        if (c != 0) continue;
         n_iter[l] += 1;
         if (jacc == 0) {
             n_roll[l] += nj;
@@ -3282,7 +3287,7 @@ static void launch_post_trial(const gym_model* m, const gym_weights* w, const gy
                                    st, Dyn(*m), kw(*w), c, io, K1, cs, b->x_ref, b->u_ref, b->cost, b->dJ,
                                    b->retry_list + rg.lo, counter, b->cand_ok, b->Bp, b->N);
         }
-        const int64_t items = sc.V > 0 ? n * ((b->N + CPK - 1) / CPK) : n;
+        const int64_t items = sc.V > 0 ? n * (1 + (b->N + CPK - 1) / CPK) : n;
         TimedLaunch tl(b->timing, 3, st);
         hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_retry), dim3(grid_for(items, BLK, POST_CAP)), dim3(BLK), 0, st, Dyn(*m),
                            kw(*w), c, io, K1, cs, b->x_ref, b->u_ref, b->cost, b->smax, b->gamma, b->status, b->n_iter,
