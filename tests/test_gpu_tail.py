@@ -163,6 +163,30 @@ def test_candidate_scratch_is_invisible(kind):
             _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"{kind} / {name}: {f}")
 
 
+@pytest.mark.parametrize("N,max_ls", [(2, 20), (37, 2), (66, 33), (203, 64)])
+def test_candidate_scratch_on_short_horizons_and_line_search_lengths(N, max_ls):
+    """The candidate scratch at the edges of its layout: one-stage and ragged horizons (the copy's knot chunks past
+    N), one candidate per lane (max_ls = 2), candidates spanning wavefronts unevenly (32 / 63 per lane), against
+    the re-run of every accepted candidate, bit for bit."""
+    from bench import load_refs
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur = load_refs()
+    xr, ur = xr[:N].copy(), ur[:N - 1].copy()
+    B, max_iters = 130, 40
+    x0 = _hard_lanes(B, seed=11)
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=1.0, max_ls=max_ls, hist_len=max_iters, pipeline=False,
+              tail_lanes=0)
+    r = BatchedNewtonSolver(eng, xr, ur, B, cand_slots=0, **kw).solve(x0, max_iters)
+    assert int((r.n_rollouts > r.n_iter).sum()) > 0            # some lane backtracked
+    s = BatchedNewtonSolver(eng, xr, ur, B, **kw)
+    assert s.cand_slots > 0
+    t = s.solve(x0, max_iters)
+    for f in FIELDS:
+        _same(getattr(t, f).cpu().numpy(), getattr(r, f).cpu().numpy(), f"N={N}, max_ls={max_ls}: {f}")
+
+
 @pytest.mark.parametrize("kind", ["pipelined", "serial", "per_lane_noreorder", "serial_single_wave"])
 def test_lane_compaction_is_invisible(kind):
     """The low-occupancy switch forced at every host synchronisation (compact="force"): lane compaction
