@@ -2618,9 +2618,10 @@ __device__ __forceinline__ void tail_trial_chain(const double* tst, tring_t ring
                 const double ysig = __builtin_fma(dg, q[5], y);             // trial_u1_sig's value
                 const double u1 = c == 0 ? y : ysig;
                 gym::rk4_pair_fast<true>(m, odd, n0, n1, n2, n3, u1, pk);   // branch-free near path, as k_nt_run2
-                double2* r = ring[cc & 1][j][tc];
-                if (odd) r[1] = make_double2(n2, n3);
-                else { r[0] = make_double2(n0, n1); r[2] = make_double2(u1, 0.0); }
+                double2* r = ring[cc & 1][j][tc];   // both lanes of the pair: the same values, no per-lane select
+                r[0] = make_double2(n0, n1);
+                r[1] = make_double2(n2, n3);
+                r[2] = make_double2(u1, 0.0);
             }
         }
         __syncthreads();
