@@ -2446,6 +2446,7 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
     const double* xr = lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N);
     const double* ur = lane_ref<RL>(R->ur, l, 2 * (int64_t)T);
     const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t so2 = lane == 0 ? o2 : 0x80000000u, so1 = lane == 0 ? o1 : 0x80000000u;   // OOB: dropped
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Kb = reinterpret_cast<const char*>(R->K1);
     const char* Cb = reinterpret_cast<const char*>(R->cs);
@@ -2489,10 +2490,8 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                                 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, dt};   // q, r: the vector half's
                     double k0, k1, k2, k3, G11, iG;
                     S.step_P(kw, L, k0, k1, k2, k3, G11, iG);
-                    if (lane == 0) {
-                        double* g = G + i * TL_GK;
-                        g[0] = k0; g[1] = k1; g[2] = k2; g[3] = k3; g[4] = G11; g[5] = iG;
-                    }
+                    double* g = G + i * TL_GK;     // every thread: the same values at the same addresses
+                    g[0] = k0; g[1] = k1; g[2] = k2; g[3] = k3; g[4] = G11; g[5] = iG;
                 }
             }
         } else {
@@ -2511,7 +2510,8 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                                 s[10], s[11], s[12], s[13], s[14], s[15], dt};
                     double s0, s1;
                     S.step_p<U0Z>(kw, L, k0, k1, k2, k3, g[4], g[5], s0, s1);
-                    if (lane == 0) {
+                    {   // every thread: the same values; lane 0's global stores land, the others' fall outside the
+                        // resources' range (dropped by the hardware) -- no exec-mask branch on the pass
                         const int ts = tb - i;
                         const double2 xa = make_double2(s[16], s[17]), xb = make_double2(s[18], s[19]);
                         const double cg = stage_cg(xa, xb, s[20], g0, k0, k1, k2, k3, s1);
@@ -2519,10 +2519,10 @@ __device__ __forceinline__ void tail_sweep_split(double* lin3, double* gk2, doub
                         q[0] = k0; q[1] = k1; q[2] = k2; q[3] = k3; q[4] = cg; q[5] = s1;
                         const auto rC = rsrc(Cb + (int64_t)ts * row);
                         const auto rK = rsrc(Kb + (int64_t)ts * (2 * (int64_t)row));
-                        bst2(rK, o2, 0, k0, k1);
-                        bst2(rK, o2, WROW, k2, k3);
-                        bst1(rC, o1, 0, cg);
-                        bst1(rC, o1, plane, s1);
+                        bst2(rK, so2, 0, k0, k1);
+                        bst2(rK, so2, WROW, k2, k3);
+                        bst1(rC, so1, 0, cg);
+                        bst1(rC, so1, plane, s1);
                     }
                 }
             }

@@ -27,6 +27,7 @@ for s in "$@"; do
     tests_cand) step pytest_cand 600 $PYT tests/test_gpu_tail.py -m gpu -k "candidate_scratch" || exit $? ;;
     cand_ab) step cand_ab 400 python -u tools/cand_ab.py --rounds 3 || exit $? ;;
     tail_ab) step tail_ab 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/tail_base.so build_ab/tail_new.so || exit $? ;;
+    sw_ab) step sw_ab 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/sw_base.so build_ab/sw_new.so || exit $? ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
