@@ -2027,6 +2027,7 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
     const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t so2 = act ? o2 : 0x80000000u, so1 = act ? o1 : 0x80000000u;   // inactive: dropped (OOB)
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Kb = reinterpret_cast<const char*>(R->K1);
     const char* Cb = reinterpret_cast<const char*>(R->cs);
@@ -2054,14 +2055,13 @@ __device__ __forceinline__ void run2_sweep_vec(ring_t ring, gring_t gring, int l
                             qa.x, qa.y, qb.x, qb.y, rr.x, rr.y, dtv};
                 double s0, s1;
                 S.step_p<U0Z>(wv, L, ka01.x, ka01.y, ka23.x, ka23.y, gi.x, gi.y, s0, s1);
-                if (act) {
-                    if (ext)   // external retries: sigma1 stored too (the candidates read it; no re-run)
-                        store_stage<OUT_ALL>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
-                                             ka01.y, ka23.x, ka23.y, s1);
-                    else
-                        store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, o2, o1, xa, xb, uu.y, g0, ka01.x,
-                                                ka01.y, ka23.x, ka23.y, s1);
-                }
+                // an inactive lane's stores take an offset past the resources' range (dropped): no exec-mask branch
+                if (ext)   // external retries: sigma1 stored too (the candidates read it; no re-run)
+                    store_stage<OUT_ALL>(Kb, Cb, T - 1 - i, row, plane, so2, so1, xa, xb, uu.y, g0, ka01.x,
+                                         ka01.y, ka23.x, ka23.y, s1);
+                else
+                    store_stage<OUT_SOLVER>(Kb, Cb, T - 1 - i, row, plane, so2, so1, xa, xb, uu.y, g0, ka01.x,
+                                            ka01.y, ka23.x, ka23.y, s1);
             }
         }
         lds_barrier(bw);
@@ -2187,6 +2187,7 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
     const int T = R->N - 1;
     const int64_t Bp = R->Bp;
     const uint32_t o2 = wbo(l, 2), o1 = (uint32_t)l * 8u;
+    const uint32_t so2 = act ? o2 : 0x80000000u, so1 = act ? o1 : 0x80000000u;   // inactive: dropped (OOB)
     const uint32_t row = (uint32_t)Bp * 16u, plane = (uint32_t)Bp * 8u;
     const char* Ub = reinterpret_cast<const char*>(R->u[cb]);
     const char* Xb = reinterpret_cast<const char*>(R->x[cb ^ 1]);
@@ -2220,13 +2221,13 @@ __device__ __forceinline__ double run2_trial_helper(ring_t ring, int lane, int64
                 const double v1 = vv.x;
                 const double f0 = U0Z ? 0.0 : v0 - urt.v[0], f1 = v1 - urt.v[1];
                 J = stage_cost<U0Z>(J, ka.w.Q, ka.w.R, n0, n1, n2, n3, xrt.v, f0, f1);
-                if (act) {
+                {   // an inactive lane's stores fall outside the resources' range (dropped): no exec-mask branch
                     const auto rO = rsrc(Ob + (int64_t)t * row);
-                    if (!U0Z) bst1(rO, o1, 0, v0);
-                    bst1(rO, o1, plane, v1);
+                    if (!U0Z) bst1(rO, so1, 0, v0);
+                    bst1(rO, so1, plane, v1);
                     const auto rX = rsrc(Xb + (int64_t)(t + 1) * (2 * (int64_t)row));
-                    bst2(rX, o2, 0, na.x, na.y);
-                    bst2(rX, o2, WROW, nb.x, nb.y);
+                    bst2(rX, so2, 0, na.x, na.y);
+                    bst2(rX, so2, WROW, nb.x, nb.y);
                 }
                 n0 = na.x; n1 = na.y; n2 = nb.x; n3 = nb.y;
             }

@@ -28,6 +28,9 @@ for s in "$@"; do
     cand_ab) step cand_ab 400 python -u tools/cand_ab.py --rounds 3 || exit $? ;;
     tail_ab) step tail_ab 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/tail_base.so build_ab/tail_new.so || exit $? ;;
     sw_ab) step sw_ab 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/sw_base.so build_ab/sw_new.so || exit $? ;;
+    r2_ab) step r2_ab_cfg2 300 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --batch 4096 --rounds 5 build_ab/r2_base.so:run build_ab/r2_new.so:run &&
+           step r2_ab_stress 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/r2_base.so build_ab/r2_new.so || exit $? ;;
+    r2_ab_run) step r2_ab_cfg2 300 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --batch 4096 --rounds 5 build_ab/r2_base.so:run build_ab/r2_new.so:run || exit $? ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
