@@ -31,6 +31,7 @@ for s in "$@"; do
     r2_ab) step r2_ab_cfg2 300 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --batch 4096 --rounds 5 build_ab/r2_base.so:run build_ab/r2_new.so:run &&
            step r2_ab_stress 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/r2_base.so build_ab/r2_new.so || exit $? ;;
     r2_ab_run) step r2_ab_cfg2 300 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --batch 4096 --rounds 5 build_ab/r2_base.so:run build_ab/r2_new.so:run || exit $? ;;
+    th_ab) step th_ab 500 env GYM_ALLOW_FOREIGN_BUILD=1 python -u tools/ab_bench.py --spread 1.5 --rounds 3 build_ab/th_base.so build_ab/th_new.so || exit $? ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
