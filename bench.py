@@ -194,7 +194,7 @@ class NewtonLeg:
     """One timed configuration of the batched solver on this rank: ``total`` global lanes of the bench workload,
     this rank's contiguous shard, the schedule chosen on the largest shard (identical on every rank)."""
 
-    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None, spread=None):
+    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None, spread=None, **solver_kw):
         from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
         self.rank, self.world = gd.rank_world()
         self.total = int(total)
@@ -206,7 +206,7 @@ class NewtonLeg:
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
             schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
             split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes, world_size=self.world,
-            compact=None if a.compact == "auto" else a.compact == "on")
+            compact=None if a.compact == "auto" else a.compact == "on", **solver_kw)
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
@@ -214,7 +214,7 @@ class NewtonLeg:
         self.reduce = gd.TimedReduce(base) if base is not None else None
         self.a, self.gd = a, gd
 
-    def run(self, steps: int, warmup: int):
+    def run(self, steps: int, warmup: int, box=None):
         import torch
         a, gd, solver = self.a, self.gd, self.solver
         for _ in range(warmup):
@@ -222,33 +222,43 @@ class NewtonLeg:
         solver.reset_timing()
         if self.reduce is not None:
             self.reduce.reset()
+        smi0 = box.smi() if box is not None else None       # outside the timed region (an amd-smi call, ~0.3 s)
         gd.barrier()
         torch.cuda.synchronize()
+        if box is not None:
+            box.mark()
         t0 = time.perf_counter()
         lane_its, rolls, res, tail_its, compactions, lowocc_its = 0, 0, None, 0, 0, 0
+        tail_iters_max = 0
         for _ in range(steps):
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
             lane_its += res.lane_iterations
             rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
             tail_its += res.tail_lane_iterations
+            tail_iters_max = max(tail_iters_max, res.tail_iterations)
             compactions += res.compactions
             lowocc_its += res.lowocc_lane_iterations
         torch.cuda.synchronize()
         local = time.perf_counter() - t0       # this rank's own time, before waiting for the others
+        win = box.window() if box is not None else None    # sysfs samples only: no delay
         gd.barrier()
         elapsed = gd.max_over_ranks(time.perf_counter() - t0)
+        self.box = box.summary(win, smi0, box.smi()) if box is not None else None
         red = self.reduce
         self.rank_records = gd.gather_floats([local, lane_its, red.reduce_s if red else 0.0,
                                               red.readback_s if red else 0.0, red.calls if red else 0,
                                               res.iterations if res is not None else 0])
         self.res, self.lane_its, self.steps, self.tail_lane_its = res, lane_its, steps, tail_its
+        self.tail_iters_max = tail_iters_max
         self.compactions = compactions
         self.lowocc_lane_its = lowocc_its
         self.elapsed = elapsed
         self.lane_its_all = int(gd.sum_over_ranks(lane_its))
         self.rollouts_all = int(gd.sum_over_ranks(rolls))
         self.value = self.lane_its_all / elapsed
+        if self.box is not None and self.box.get("energy_j"):
+            self.box["uj_per_lane_iteration"] = round(1e6 * self.box["energy_j"] / max(lane_its, 1), 3)
         return self
 
     def kernel_report(self, N: int):
@@ -307,6 +317,76 @@ class NewtonLeg:
         import torch
         self.solver = self.res = self.x0_dev = None
         torch.cuda.empty_cache()
+
+
+class BoxMonitor:
+    """The box state of this rank's GPU during each timed leg (tools/box_state.py): SCLK / MCLK DPM levels, power
+    against its cap, junction and memory temperatures (sysfs, sampled every 0.1 s on a background thread, mean / min /
+    max over the leg's timed region), and from amd-smi's accumulated counters the share of the region spent under the
+    power cap (PPT) or a thermal limit and the energy it used.  File reads and one amd-smi call outside each timed
+    region; nothing touches the GPU."""
+
+    KEYS = {"dpm_sclk_mhz": "sclk_mhz", "dpm_mclk_mhz": "mclk_mhz", "dpm_fclk_mhz": "fclk_mhz",
+            "power_ppt_in_w": "power_w", "power_ppt_avg_w": "power_avg_w", "power_cap_w": "power_cap_w",
+            "temp_junction_c": "temp_junction_c", "temp_hotspot_c": "temp_hotspot_c", "temp_mem_c": "temp_mem_c",
+            "temp_edge_c": "temp_edge_c"}
+
+    def __init__(self, device_index: int = 0, use_smi: bool = True):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import box_state
+        self._bs = box_state
+        self.use_smi = use_smi          # amd-smi's first GPU is this process's only on a one-GPU box
+        self.s = box_state.Sampler(device_index, 0.1).start()
+
+    def mark(self):
+        self.s.mark()
+
+    def window(self):
+        return self.s.window()
+
+    def smi(self):
+        return self._bs.smi_counters(20.0) if self.use_smi else {}
+
+    def summary(self, win, smi0, smi1) -> dict:
+        out = {self.KEYS[k]: v for k, v in win.items() if k in self.KEYS}
+        if "power_cap_w" in out:
+            out["power_cap_w"] = out["power_cap_w"][0]
+        out.update(self._bs.smi_delta(smi0 or {}, smi1 or {}))
+        out["samples"] = win.get("samples", 0)
+        return out
+
+    def stop(self):
+        self.s.stop()
+
+
+def stress_tail_record(leg, ks, T: int) -> dict:
+    """The straggler tail of the stress leg and the bound it sets (SURVEY 8(d) stress variant).
+
+    The tail runs every remaining lane's iterations in one workgroup per lane, so a tail launch lasts as long as its
+    slowest lane: its seconds over the outer iterations it ran are one lane-iteration's latency on the critical path
+    (a sweep pass and the Armijo trials, T stages each).  critical_path_s = the longest lane's iteration count x that
+    latency: the solve time if every iteration of the batch's slowest lane ran at the tail's single-lane speed, i.e.
+    the floor one lane running to max_iters sets with today's chains; frac_of_critical_path = critical_path_s / the
+    measured seconds per solve (1 = the solve is that one lane's chain and nothing else)."""
+    steps = max(leg.steps, 1)
+    rec = {"launches_per_step": leg.solver.launches["tail"] / steps,
+           "share_of_lane_iterations": leg.tail_lane_its / max(leg.lane_its, 1), "seconds_per_step": None}
+    if not ks or "tail" not in ks or not leg.tail_iters_max:
+        return rec
+    tail_s = ks["tail"]["avg_ms"] * ks["tail"]["launches"] / 1e3 / steps
+    lat = tail_s / leg.tail_iters_max
+    n_max = int(leg.res.n_iter.max().item())
+    solve_s = leg.elapsed / steps
+    rec.update({"seconds_per_step": tail_s, "from_iteration": leg.res.tail_from_iteration,
+                "outer_iterations_per_step": leg.tail_iters_max, "lane_iteration_latency_ms": 1e3 * lat,
+                "max_lane_iterations": n_max, "critical_path_s": n_max * lat,
+                "frac_of_critical_path": n_max * lat / solve_s,
+                "share_of_solve": tail_s / solve_s})
+    sclk = (leg.box or {}).get("sclk_mhz")
+    if sclk:
+        # cycles per stage of one tail lane-iteration (one sweep stage + one trial stage) at the leg's SCLK range
+        rec["cycles_per_stage_at_sclk"] = {"mean": lat * sclk[0] * 1e6 / T, "max": lat * sclk[2] * 1e6 / T}
+    return rec
 
 
 def outcome_record(res) -> dict:
@@ -392,6 +472,8 @@ def main():
     ap.add_argument("--numpy-iters", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--no-box", action="store_true", help="skip the box-state record (sysfs clocks / power / "
+                                                            "temperatures, amd-smi throttle and energy counters)")
     ap.add_argument("--sync-every", type=int, default=4,
                     help="outer iterations between host reads of the (all-reduced) statistics; iterations "
                          "enqueued after every lane has finished are no-ops")
@@ -474,8 +556,9 @@ def main():
     strong = a.global_batch is not None
     total = a.global_batch if strong else a.batch * world
     eng = AcrobotEngine()
+    box = None if a.no_box or rank != 0 else BoxMonitor(gd.local_device_index(local_rank), use_smi=world == 1)
     main_leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing,
-                         u0_zero=False if a.u0_zero == "off" else None).run(a.steps, a.warmup)
+                         u0_zero=False if a.u0_zero == "off" else None).run(a.steps, a.warmup, box)
     res = main_leg.res
     value = main_leg.value
 
@@ -572,8 +655,10 @@ def main():
 
     # secondary legs (same process, same JSON line)
     legs = [s for s in a.extra_legs.split(",") if s] if a.workload == "newton" else []
+    box_legs = {"main": main_leg.box}
     if "cfg4" in legs and not strong:
-        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG4_LANES, not a.no_timing).run(a.extra_steps, 1)
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG4_LANES, not a.no_timing).run(a.extra_steps, 1, box)
+        box_legs["strong_scaling_cfg4"] = leg.box
         k4, r4 = leg.kernel_report(N)
         out["strong_scaling_cfg4"] = {
             "value": leg.value, "unit": "Newton iterations/s", "scaling": "strong", "global_lanes": CFG4_LANES,
@@ -585,7 +670,8 @@ def main():
                     "host sync); max-over-ranks wall time"}
         leg.free()
     if "general" in legs and world == 1 and a.u0_zero == "auto":
-        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, u0_zero=False).run(a.extra_steps, 1)
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, u0_zero=False).run(a.extra_steps, 1, box)
+        box_legs["general_path"] = leg.box
         kg, rg = leg.kernel_report(N)
         out["general_path"] = {
             "value": leg.value, "unit": "Newton iterations/s", "steps": a.extra_steps, "warmup": 1,
@@ -600,7 +686,8 @@ def main():
         leg.free()
 
     if "cfg2" in legs and world == 1 and (strong or a.batch != CFG2_LANES):
-        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG2_LANES, not a.no_timing).run(a.extra_steps, 1)
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG2_LANES, not a.no_timing).run(a.extra_steps, 1, box)
+        box_legs["cfg2"] = leg.box
         k2, r2 = leg.kernel_report(N)
         out["cfg2"] = {
             "value": leg.value, "unit": "Newton iterations/s", "lanes": CFG2_LANES, "steps": a.extra_steps,
@@ -613,7 +700,8 @@ def main():
     if "stress" in legs and world == 1:
         # SURVEY 8(d)'s stress variant: the cfg 3 batch with th ~ U(+-1.5): backtracking, Armijo failures and a
         # straggler tail; the automatic schedule (pipelined -> lane compaction / low-occupancy regime -> tail)
-        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, spread=1.5).run(a.extra_steps, 1)
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing, spread=1.5).run(a.extra_steps, 1, box)
+        box_legs["stress"] = leg.box
         ks, rs = leg.kernel_report(N)
         sv = leg.solver
         out["stress"] = {
@@ -622,10 +710,7 @@ def main():
             "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
             "rollouts_per_s": leg.rollouts_all / leg.elapsed,
             "roofline": None if rs is None else {k: rs[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
-            "straggler_tail": {"launches_per_step": sv.launches["tail"] / a.extra_steps,
-                               "share_of_lane_iterations": leg.tail_lane_its / max(leg.lane_its, 1),
-                               "seconds_per_step": None if not ks or "tail" not in ks else
-                               ks["tail"]["avg_ms"] * ks["tail"]["launches"] / 1e3 / a.extra_steps},
+            "straggler_tail": stress_tail_record(leg, ks, T),
             "low_occupancy": {"from_iteration": sv.serial_switch_at, "compactions_per_step":
                               leg.compactions / a.extra_steps,
                               "share_of_lane_iterations": leg.lowocc_lane_its / max(leg.lane_its, 1)},
@@ -641,6 +726,14 @@ def main():
                                              "roofline", "parity")}
         out["mpc_cfg5"]["note"] = "BASELINE cfg 5 (--workload mpc makes it the main line, with its CPU baseline)"
 
+    if box is not None:
+        box.stop()
+        out["box"] = {"sysfs": box.s.dev, "legs": box_legs, "note": (
+            "this GPU during each leg's timed region: DPM SCLK / MCLK / FCLK (MHz), power and its cap (W), junction and "
+            "HBM temperatures (C) as [mean, min, max] of sysfs samples every 0.1 s; ppt_share / *_thermal_share: share "
+            "of the region the SMU spent limited by the package power cap / a thermal limit (amd-smi throttle "
+            "counters), energy_j and uj_per_lane_iteration from its energy counter.  A leg at power = cap with "
+            "ppt_share near 1 runs at the SCLK the cap allows (DESIGN 6)")}
     if rank == 0 and world == 1 and not a.no_cpu:
         x0_all = make_x0(total, spread=a.spread)
         out["cpu_baseline"] = cpu_baseline(x0_all, x_ref, u_ref, a.cpu_lanes, a.max_iters)

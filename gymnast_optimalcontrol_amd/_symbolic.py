@@ -22,8 +22,11 @@ INPUT_SYMBOLS = ("tau1", "tau2")
 
 
 def _entries(sp, s):
-    """The reference's module-level scalar entries M11 .. M22, C11 .. C22, G1, G2 (dynamics.py:64-83), unsimplified
-    as the reference leaves them (M and Gvec simplify them entry by entry)."""
+    """The reference's module-level scalar entries M11 .. M22, C11 .. C22, G1, G2 (dynamics.py:64-83), unsimplified.
+    They are mathematically equal to the reference's entries, not structurally: the factoring differs (e.g. G1 is
+    g (m1 lc1 + m2 l1) sin(th1) + ..., M12 is d + h cos(th2)), so ``==`` / ``str()`` / ``.args`` comparisons against
+    the reference's trees differ while ``simplify(a - b) == 0`` holds (tests/test_abi_host.py checks that).  M and
+    Gvec simplify them entry by entry, as the reference does."""
     c2, s2 = sp.cos(s["theta2"]), sp.sin(s["theta2"])
     h = s["l1"] * s["lc2"] * s["m2"]                       # the coupling coefficient m2 l1 lc2
     d = s["I2"] + s["m2"] * s["lc2"] ** 2

@@ -94,6 +94,11 @@ def make_reduce_stats(group=None, force: bool = False):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         return t
 
+    def max_of(value: float) -> float:
+        """MAX over ranks of a host scalar (the straggler-tail switch's per-rank active count)."""
+        return max_over_ranks(value, group=group, force=force)
+
+    reduce_stats.max_of = max_of
     return reduce_stats
 
 
@@ -106,6 +111,7 @@ class TimedReduce:
 
     def __init__(self, reduce):
         self.reduce = reduce
+        self.max_of = getattr(reduce, "max_of", None)
         self.reduce_s = 0.0
         self.readback_s = 0.0
         self.calls = 0

@@ -65,6 +65,8 @@ class SolveResult:
     tail_lane_iterations: int = 0           # lane-iterations run by the straggler tail (gym_newton_tail)
     compactions: int = 0                    # lane compactions during the loop (BatchedNewtonSolver.compact)
     lowocc_lane_iterations: int = 0         # lane-iterations run in the low-occupancy regime (maybe_compact)
+    tail_from_iteration: int | None = None  # the outer iteration the straggler tail took over at (None: no tail)
+    tail_iterations: int = 0                # outer iterations the tail ran (its slowest lane's, up to the last one)
 
 
 class BatchedNewtonSolver:
@@ -220,9 +222,15 @@ class BatchedNewtonSolver:
         # Default: on with the automatic schedule choice, TAIL_LANES_PER_CU per CU of every rank (``world_size``:
         # the ranks the statistics are all-reduced over, so the switch comes at the same per-GPU occupancy at any
         # world size); a caller that picks a schedule gets it pure
+        # the default also caps each rank's own active count at its per-GPU budget (tail_lanes_rank; the maximum over
+        # ranks is all-reduced once the global count is under the threshold): with skewed shards one rank could
+        # otherwise enter the tail with up to world x its budget of lanes, one workgroup each
+        self.tail_lanes_rank = None
         if tail_lanes is None:
-            tail_lanes = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count *
-                          max(int(world_size), 1) if auto_schedule else 0)
+            per_rank = (self.TAIL_LANES_PER_CU * torch.cuda.get_device_properties(dev).multi_processor_count
+                        if auto_schedule else 0)
+            tail_lanes = per_rank * max(int(world_size), 1)
+            self.tail_lanes_rank = per_rank or None
         # the tail kernel's limits: at most 64 trials, horizons up to its LDS staging, and that LDS within the
         # device's opt-in limit (checked here, so a device with less LDS turns the tail off instead of failing mid-solve)
         need, lds, lds_max = C.c_int64(), C.c_int64(), C.c_int64()
@@ -251,21 +259,33 @@ class BatchedNewtonSolver:
         # instead of re-run (a T-step chain per backtracking iteration).  Slots for min(lanes x (max_ls - 1),
         # cand_slots) candidates (~24 KiB each at T = 500); lanes past them are re-run.  The straggler tail borrows
         # the same buffer.  0 turns it off (the same bits either way).
+        # Allocated on demand (ensure_cand_scratch): at the first host synchronisation whose iteration had lanes
+        # rejecting trial 1, on entering the low-occupancy regime, or for the tail; a solve in which no lane
+        # backtracks (the headline workload) never holds it.  Until then the accepted candidates are re-run (the
+        # same bits).
         if cand_slots is None:
             cand_slots = self.CAND_SLOTS
         slots = min(self.Bp * max(int(max_ls) - 1, 0), int(cand_slots))
         slots = slots // 64 * 64
         self._cand_scratch = None
-        if (slots > 0 and not self.persistent and not self.checkpoint and self.split_waves):
-            need = C.c_int64()
-            _lib.check(engine.lib.gym_newton_cand_scratch(self.N, slots, C.byref(need)), "gym_newton_cand_scratch")
-            self._cand_scratch = torch.empty(int(need.value), dtype=F64, device=dev)
-            b.cand_scratch, b.cand_slots = self._cand_scratch.data_ptr(), slots
-        self.cand_slots = slots if self._cand_scratch is not None else 0
+        ok = slots > 0 and not self.persistent and not self.checkpoint and self.split_waves
+        self.cand_slots = slots if ok else 0
         self.tail_lane_its = 0
+        self.tail_from, self.tail_iters = None, 0
         self._cap_pos = None
         self._cap_log = []
         self._sig_log = []
+
+    def ensure_cand_scratch(self) -> bool:
+        """Allocate the candidate scratch (cand_slots slots, ~24 KiB each at T = 500) if this solver uses one and has
+        not yet; stream-ordered, so the next launch may use it.  Returns whether it is in place."""
+        if self._cand_scratch is None and self.cand_slots > 0:
+            need = C.c_int64()
+            _lib.check(self.eng.lib.gym_newton_cand_scratch(self.N, self.cand_slots, C.byref(need)),
+                       "gym_newton_cand_scratch")
+            self._cand_scratch = torch.empty(int(need.value), dtype=F64, device=self.eng.device)
+            self.batch.cand_scratch, self.batch.cand_slots = self._cand_scratch.data_ptr(), self.cand_slots
+        return self._cand_scratch is not None
 
     @property
     def schedule(self) -> str:
@@ -345,6 +365,7 @@ class BatchedNewtonSolver:
         need = C.c_int64()
         _lib.check(self.eng.lib.gym_newton_tail_scratch(self.N, n, int(self.armijo.max_ls), C.byref(need)),
                    "gym_newton_tail_scratch")
+        self.ensure_cand_scratch()
         if self._cand_scratch is not None and self._cand_scratch.numel() >= need.value:
             sc = self._cand_scratch          # the candidate scratch (the tail and the post-trial kernels never overlap)
         else:
@@ -540,6 +561,7 @@ class BatchedNewtonSolver:
         trial 1 finished by the serial schedule's parallel candidates and accepted re-run (GYM_FLAG_SIGMA_STREAM);
         with single-wavefront persistent kernels (split_waves=False), on the serial schedule (its sweep storing
         sigma1).  The same bits either way (the schedules' bitwise equality)."""
+        self.ensure_cand_scratch()
         if not self._serial_now:
             self.serial_switch_at = self.k
             self._its_switch = int(self.n_iter[:self.B].sum().item())
@@ -619,6 +641,7 @@ class BatchedNewtonSolver:
             inv[perm] = torch.arange(self.B, device=perm.device)
             self._capture_start(inv[torch.as_tensor(self.capture_lanes, device=perm.device)].tolist())
         self.tail_lane_its = 0
+        self.tail_from, self.tail_iters = None, 0
         self.compactions = 0
         self._compact_prev = None
         self.serial_switch_at = None
@@ -660,6 +683,8 @@ class BatchedNewtonSolver:
         res["sigmas"] = self.captured_sigmas() if self.capture_lanes is not None else None
         res["schedule"] = self.schedule
         res["tail_lane_iterations"] = int(self.tail_lane_its)
+        res["tail_from_iteration"] = self.tail_from
+        res["tail_iterations"] = int(self.tail_iters)
         res["compactions"] = int(self.compactions)
         lowocc = 0
         if self.serial_switch_at is not None:   # up to the tail switch, or the end of the solve
@@ -752,14 +777,34 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
                       f"retry={int(host[4])}", flush=True)
             if host[0] == 0:
                 break
+            if host[4] > 0:   # lanes rejected trial 1: from now on the post-trial search records its candidates
+                ensure = getattr(stepper, "ensure_cand_scratch", None)
+                if ensure is not None:
+                    ensure()
             # the straggler tail: decided on the (all-reduced) global active count, so every rank switches at the
-            # same iteration and pairs up the same collectives afterwards
-            if tail and host[0] <= tail and k + 1 < max_iters:
+            # same iteration and pairs up the same collectives afterwards; with a per-rank budget (tail_lanes_rank)
+            # also on the largest rank's own count, all-reduced (MAX) by every rank at the same iteration (they all
+            # see the same global count)
+            if tail and host[0] <= tail and k + 1 < max_iters and _tail_rank_ok(stepper, host, local, reduce_stats):
                 log += tail_loop(stepper, k + 1, int(max_iters), reduce_stats, log_every, keep_stats)
                 break
             if compact is not None and k + 1 < max_iters:   # rank-local: no collective depends on it
                 compact(int(local[0].item()) if reduce_stats is not None else int(host[0]))
     return log
+
+
+def _tail_rank_ok(stepper, host, local, reduce_stats) -> bool:
+    """The per-rank part of the straggler-tail switch: the largest rank's active count within ``tail_lanes_rank``
+    (None: no per-rank budget).  Sharded, the maximum is one MAX all-reduce (``reduce_stats.max_of``) that every rank
+    issues at the same iteration; a reduce without it compares the global count (>= every rank's) instead."""
+    cap = getattr(stepper, "tail_lanes_rank", None)
+    if cap is None:
+        return True
+    if reduce_stats is None:
+        return host[0] <= cap
+    max_of = getattr(reduce_stats, "max_of", None)
+    n = float(local[0].item()) if isinstance(local, torch.Tensor) else float(np.asarray(local)[0])
+    return (max_of(n) if max_of is not None else host[0]) <= cap
 
 
 def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep_stats: bool) -> list:
@@ -792,6 +837,7 @@ def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep
     # reports its global count (a rank-local maximum would differ between ranks)
     if reduce_stats is None and solver.B:
         solver.k = max(k_switch, min(solver.k, int(solver.n_iter[:solver.B].max().item())))
+    solver.tail_from, solver.tail_iters = k_switch, solver.k - k_switch
     return log
 
 

@@ -153,14 +153,17 @@ typedef struct gym_batch {
     const int64_t* lane_map; /* optional (B): lane i's results go to row lane_map[i] of the lane-major outputs
                          * of gym_newton_finalize / gym_newton_sigma (a permutation; NULL: identity)  */
     gym_timing* timing; /* [host] optional kernel timing (NULL: none)               */
-    /* optional (ABI 13) candidate scratch of the post-trial Armijo search (gym_newton_iteration / _phase / _run with
-     * GYM_FLAG_SIGMA_STREAM): candidate i = r (max_ls - 1) + j - 1 (retry-list entry r, step gamma0 beta^j) stores
+    /* optional (ABI 13) candidate scratch of the post-trial Armijo search.  Used by every post-trial launch when
+     * cand_slots > 0 and neither GYM_FLAG_X_CKPT nor GYM_FLAG_RUN_SINGLE is set: gym_newton_iteration and
+     * gym_newton_phase always, gym_newton_run when GYM_FLAG_SIGMA_STREAM sends its retries to the post-trial search
+     * (a caller must not hand over a buffer it expects untouched on those paths).  Candidate i = r (max_ls - 1) + j - 1 (retry-list entry r, step gamma0 beta^j) stores
      * its trajectory, controls and cost in slot i while i < cand_slots, and the accepted one is then copied into
      * the lane's next iterate instead of re-running its rollout (a chain of T RK4 steps); candidates without a
      * slot are re-run as before.  cand_scratch: gym_newton_cand_scratch(N, cand_slots) doubles, laid out as
      * x (N, V/64, 2, 64) double2 | u (T, 2, V) planes | J (V), V = cand_slots (a multiple of 64).
-     * cand_slots = 0 (or NULL): every accepted candidate is re-run.  Not used with GYM_FLAG_X_CKPT or
-     * GYM_FLAG_RUN_SINGLE (their candidates keep the single-lane re-run path).  Bits are the same either way. */
+     * cand_slots = 0 (or NULL): every accepted candidate is re-run.  With GYM_FLAG_X_CKPT or GYM_FLAG_RUN_SINGLE
+     * the candidates keep the single-lane re-run path and the buffer is not touched.  Bits are the same either way;
+     * the caller may install it between launches (the Python solver does so on demand). */
     double* cand_scratch;
     int64_t cand_slots;
 } gym_batch;

@@ -288,6 +288,48 @@ def test_tail_switch_is_global_across_ranks(tmp_path):
     assert g[0]["n_iter"] == [5, 60, 61] and g[1]["n_iter"] == [100, 7, 8, 9]
 
 
+def _tail_budget_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from gymnast_optimalcontrol_amd import distributed as gd
+    from gymnast_optimalcontrol_amd.solver import newton_loop
+    from host_loop_mock import MockSolver
+    gd.init_process_group(backend="gloo")
+    need = {0: [5, 60, 61, 62], 1: [7, 8, 9, 100]}[rank]   # skewed: rank 0 holds three stragglers
+    s = MockSolver(need, tail_lanes=4, tail_chunk=16)
+    s.tail_lanes_rank = 2                                  # the solver's default: a per-GPU budget
+    red = gd.TimedReduce(gd.make_reduce_stats())           # forwards max_of, as bench.py's wrapper does
+    newton_loop(s, 5000, reduce_stats=red, sync_every=4)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, dict(events=s.events, calls=red.calls, n_iter=s.n_iter.numpy().tolist()))
+    if rank == 0:
+        import json
+        with open(out_path, "w") as f:
+            json.dump(gathered, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tail_switch_waits_for_every_rank_within_its_budget(tmp_path):
+    """with skewed shards the global count can be under the threshold while one rank still holds more
+    than its per-GPU budget of active lanes; the switch then waits (one MAX all-reduce of the local counts, issued by
+    every rank at the same iteration) until the largest rank is within it."""
+    import json
+    out = str(tmp_path / "tail_budget.json")
+    mp.start_processes(_tail_budget_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    g = json.load(open(out))
+    t0 = [tuple(e) for e in g[0]["events"] if e[0] == "tail"]
+    t1 = [tuple(e) for e in g[1]["events"] if e[0] == "tail"]
+    # after k = 12: global 3 + 1 = 4 <= 4 but rank 0 holds 3 > 2; after k = 60: 2 + 1, max 2 -> both switch at 60
+    assert t0 == t1 and t0[0] == ("tail", 60, 76)
+    assert g[0]["calls"] == g[1]["calls"]
+    assert g[0]["n_iter"] == [5, 60, 61, 62] and g[1]["n_iter"] == [7, 8, 9, 100]
+
+
 def _timed_worker(rank, world, port, out_path):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
