@@ -260,9 +260,139 @@ __device__ __forceinline__ double riccati_map_lane(double P, const MapLane& c, d
 
 constexpr int kMpcMaxStages = 256;   // LDS stage table of one workgroup: its 4 windows' stages (L + 2 <= 256)
 
+// ------------------------------------------------------------------------------------------
+// compute_P_inf (:144-165) by doubling (the structure-preserving doubling algorithm for the DARE,
+// P = Q + A'PA - A'PB (R + B'PB)^-1 B'PA):  A_0 = A, G_0 = B R^-1 B', H_0 = Q, and with W = (I + G_k H_k)^-1
+//   A_{k+1} = A_k W A_k,   G_{k+1} = G_k + A_k W G_k A_k',   H_{k+1} = H_k + A_k' H_k W A_k,
+// H_k is the reference's fixed-point iterate after 2^k maps from P = Q (the horizon doubles each step), so ~10
+// doublings reach what the reference's loop reaches in ~434 dependent maps (the cfg 5 pad: P[0][0] ~ 2.26e7; the
+// reference stops where max|dP| < 1e-6, within ~9e-13 relative of the limit; the doubling lands on the limit).
+// One lane, 4x4 matrices in registers; every workgroup computes the same bits.
+// ------------------------------------------------------------------------------------------
+constexpr int kSdaMaxSteps = 40;
+
+__device__ __forceinline__ void mm44(const double* X, const double* Y, double* Z) {   // Z = X Y
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            Z[4 * i + j] = ((X[4 * i] * Y[j] + X[4 * i + 1] * Y[4 + j]) + X[4 * i + 2] * Y[8 + j]) + X[4 * i + 3] * Y[12 + j];
+}
+__device__ __forceinline__ void mm44_bt(const double* X, const double* Y, double* Z) {   // Z = X Y'
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            Z[4 * i + j] = ((X[4 * i] * Y[4 * j] + X[4 * i + 1] * Y[4 * j + 1]) + X[4 * i + 2] * Y[4 * j + 2]) +
+                           X[4 * i + 3] * Y[4 * j + 3];
+}
+__device__ __forceinline__ void mm44_at(const double* X, const double* Y, double* Z) {   // Z = X' Y
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            Z[4 * i + j] = ((X[i] * Y[j] + X[4 + i] * Y[4 + j]) + X[8 + i] * Y[8 + j]) + X[12 + i] * Y[12 + j];
+}
+
+// Inverse of a 4x4 matrix by Gauss-Jordan elimination with partial pivoting (row swaps by selects: no divergent
+// branch).  Returns false for a zero or non-finite pivot.
+__device__ __forceinline__ bool inv44(const double* M, double* Inv) {
+    double a[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[i][j] = M[4 * i + j];
+            a[i][4 + j] = i == j ? 1.0 : 0.0;
+        }
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int r = c + 1; r < 4; ++r) {        // bring the largest |a[r][c]|, r >= c, to row c
+            const bool sw = fabs(a[r][c]) > fabs(a[c][c]);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double t = a[c][k];
+                a[c][k] = sw ? a[r][k] : t;
+                a[r][k] = sw ? t : a[r][k];
+            }
+        }
+        const double p = a[c][c];
+        ok &= (p != 0.0) & (fabs(p) <= 1.7976931348623157e308);
+        const double ip = 1.0 / p;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[c][k] *= ip;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            const double f = a[r][c];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[r][k] = fma(-f, a[c][k], a[r][k]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Inv[4 * i + j] = a[i][4 + j];
+    return ok;
+}
+
+// The pad's P_inf by doubling: A_f rows 0, 1 = [1 0 h 0], [0 1 0 h], rows 2, 3 from the StageLin; B_f = [0, b],
+// b = (0, 0, b2, b3)', so G_0 = (R^-1)[1][1] b b'.  Returns the number of doublings, or 0 if they did not settle
+// (a non-finite value, or no settling within kSdaMaxSteps): the caller then runs the reference's fixed point.
+__device__ int dare_sda(double h, const double* a2, const double* a3, double b2, double b3, const M44& Q, const M22& R,
+                        double* P) {
+    double A[16] = {1.0, 0.0, h, 0.0, 0.0, 1.0, 0.0, h, a2[0], a2[1], a2[2], a2[3], a3[0], a3[1], a3[2], a3[3]};
+    const double r11 = R.v[0] / (R.v[0] * R.v[3] - R.v[1] * R.v[2]);      // (R^-1)[1][1]
+    const double bv[4] = {0.0, 0.0, b2, b3};
+    double G[16], H[16], M[16], W[16], WA[16], WG[16], T[16], U[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) G[4 * i + j] = r11 * bv[i] * bv[j];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) H[k] = Q.v[k];
+    for (int step = 1; step <= kSdaMaxSteps; ++step) {
+        mm44(G, H, M);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) M[5 * i] += 1.0;
+        if (!inv44(M, W)) return 0;
+        mm44(W, A, WA);
+        mm44(W, G, WG);
+        mm44(A, WG, T);                          // A W G
+        mm44_bt(T, A, U);                        // A W G A'
+#pragma unroll
+        for (int k = 0; k < 16; ++k) G[k] += U[k];
+        mm44(H, WA, T);                          // H W A
+        mm44_at(A, T, U);                        // A' H W A
+        double d = 0.0, hm = 0.0;
+        bool fin = true;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const double hn = H[k] + U[k];
+            d = fmax(d, fabs(hn - H[k]));
+            hm = fmax(hm, fabs(hn));
+            fin &= fabs(hn) <= 1.7976931348623157e308;
+            H[k] = hn;
+        }
+        mm44(A, WA, T);                          // A W A
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A[k] = T[k];
+        if (!fin) return 0;
+        if (d <= 1e-15 * hm) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) P[k] = H[k];
+            return step;
+        }
+    }
+    return 0;
+}
+
 // Workgroup = 4 windows (16 lanes each).  1) every stage the 4 windows use, discretised, into LDS (one lane per
-// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by every group (the same
-// bits in every workgroup: no grid-wide dependency);  3) each window's recursion from P = P_inf over stages
+// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by doubling (dare_sda; the
+// reference's fixed point if it does not settle), in every workgroup (the same bits everywhere: no grid-wide
+// dependency);  3) each window's recursion from P = P_inf over stages
 // w+L-2 .. w;  its first gain is the QP's solution u0 = K x0 at control step w.
 __global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restrict__ x_ref,
                                                   const double* __restrict__ u_ref, int S,
@@ -284,16 +414,36 @@ __global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restric
         }
     }
     __syncthreads();
+    // compute_P_inf on the pad stage: by doubling on lane 0 (dare_sda), the same bits in every workgroup
+    __shared__ double sP[16];
+    __shared__ int s_sda;
+    if (ln == 0) {
+        double Pd[16];
+        const int steps = dare_sda(m.h, pad.a2, pad.a3, pad.b2, pad.b3, Q, R, Pd);
+        s_sda = steps;
+        if (steps > 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) sP[k] = Pd[k];
+        }
+    }
+    __syncthreads();
     const MapLane c = map_lane(i, j, m.h, Q, R);
-    // compute_P_inf on the pad stage, from P = Q
-    const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2, fb3 = pad.b3;
-    double P = c.Qij, K0j, K1j;
-    int it = max_iter + 1;                                // the tolerance was never met
-    for (int n = 0; n < max_iter; ++n) {
-        const double nP = riccati_map_lane(P, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
-        const bool conv = __all(fabs(nP - P) < tol);     // np.abs(P - P_prev).max() < tol (a NaN entry fails)
-        P = nP;
-        if (conv) { it = n + 1; break; }
+    double P, K0j, K1j;
+    int it;                                               // doublings (> 0), or -(fixed-point iterations)
+    if (s_sda > 0) {
+        P = sP[4 * i + j];
+        it = s_sda;
+    } else {   // the doubling did not settle (not a stabilisable pad): the reference's fixed point, from P = Q
+        const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2,
+                     fb3 = pad.b3;
+        P = c.Qij;
+        it = -(max_iter + 1);                             // the tolerance was never met
+        for (int n = 0; n < max_iter; ++n) {
+            const double nP = riccati_map_lane(P, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
+            const bool conv = __all(fabs(nP - P) < tol);  // np.abs(P - P_prev).max() < tol (a NaN entry fails)
+            P = nP;
+            if (conv) { it = -(n + 1); break; }
+        }
     }
     if (blockIdx.x == 0 && ln < 16) {
         QT_out[ln] = P;
