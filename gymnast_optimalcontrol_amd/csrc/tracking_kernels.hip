@@ -267,130 +267,103 @@ constexpr int kMpcMaxStages = 256;   // LDS stage table of one workgroup: its 4 
 // H_k is the reference's fixed-point iterate after 2^k maps from P = Q (the horizon doubles each step), so ~10
 // doublings reach what the reference's loop reaches in ~434 dependent maps (the cfg 5 pad: P[0][0] ~ 2.26e7; the
 // reference stops where max|dP| < 1e-6, within ~9e-13 relative of the limit; the doubling lands on the limit).
-// One lane, 4x4 matrices in registers; every workgroup computes the same bits.
+// On a 16-lane group as the Riccati map below: lane 4i+j owns entry (i, j) of every 4x4 matrix; each product is one
+// round through a per-group LDS scratch (one wavefront: its LDS accesses are in order, so no barrier), W by
+// Gauss-Jordan elimination with partial pivoting (every lane finds the same pivot row).  Every group of every
+// workgroup computes the same bits.
 // ------------------------------------------------------------------------------------------
 constexpr int kSdaMaxSteps = 40;
 
-__device__ __forceinline__ void mm44(const double* X, const double* Y, double* Z) {   // Z = X Y
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            Z[4 * i + j] = ((X[4 * i] * Y[j] + X[4 * i + 1] * Y[4 + j]) + X[4 * i + 2] * Y[8 + j]) + X[4 * i + 3] * Y[12 + j];
+__device__ __forceinline__ void wave_lds_order() {   // LDS writes of this wavefront visible to its later reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void mm44_bt(const double* X, const double* Y, double* Z) {   // Z = X Y'
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            Z[4 * i + j] = ((X[4 * i] * Y[4 * j] + X[4 * i + 1] * Y[4 * j + 1]) + X[4 * i + 2] * Y[4 * j + 2]) +
-                           X[4 * i + 3] * Y[4 * j + 3];
+// (X Y)[i][j], (X Y')[i][j], (X' Y)[i][j] from 16-double LDS matrices (row-major)
+__device__ __forceinline__ double dot_xy(const double* X, const double* Y, int i, int j) {
+    return ((X[4 * i] * Y[j] + X[4 * i + 1] * Y[4 + j]) + X[4 * i + 2] * Y[8 + j]) + X[4 * i + 3] * Y[12 + j];
 }
-__device__ __forceinline__ void mm44_at(const double* X, const double* Y, double* Z) {   // Z = X' Y
+__device__ __forceinline__ double dot_xyt(const double* X, const double* Y, int i, int j) {
+    return ((X[4 * i] * Y[4 * j] + X[4 * i + 1] * Y[4 * j + 1]) + X[4 * i + 2] * Y[4 * j + 2]) + X[4 * i + 3] * Y[4 * j + 3];
+}
+__device__ __forceinline__ double dot_xty(const double* X, const double* Y, int i, int j) {
+    return ((X[i] * Y[j] + X[4 + i] * Y[4 + j]) + X[8 + i] * Y[8 + j]) + X[12 + i] * Y[12 + j];
+}
+__device__ __forceinline__ double grp16_max(double v) {   // max over the lane's 16-lane group
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            Z[4 * i + j] = ((X[i] * Y[j] + X[4 + i] * Y[4 + j]) + X[8 + i] * Y[8 + j]) + X[12 + i] * Y[12 + j];
+    for (int o = 8; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 16));
+    return v;
 }
 
-// Inverse of a 4x4 matrix by Gauss-Jordan elimination with partial pivoting (row swaps by selects: no divergent
-// branch).  Returns false for a zero or non-finite pivot.
-__device__ __forceinline__ bool inv44(const double* M, double* Inv) {
-    double a[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            a[i][j] = M[4 * i + j];
-            a[i][4 + j] = i == j ? 1.0 : 0.0;
-        }
-    bool ok = true;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int r = c + 1; r < 4; ++r) {        // bring the largest |a[r][c]|, r >= c, to row c
-            const bool sw = fabs(a[r][c]) > fabs(a[c][c]);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const double t = a[c][k];
-                a[c][k] = sw ? a[r][k] : t;
-                a[r][k] = sw ? t : a[r][k];
-            }
-        }
-        const double p = a[c][c];
-        ok &= (p != 0.0) & (fabs(p) <= 1.7976931348623157e308);
-        const double ip = 1.0 / p;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a[c][k] *= ip;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (r == c) continue;
-            const double f = a[r][c];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[r][k] = fma(-f, a[c][k], a[r][k]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Inv[4 * i + j] = a[i][4 + j];
-    return ok;
-}
-
-// The pad's P_inf by doubling: A_f rows 0, 1 = [1 0 h 0], [0 1 0 h], rows 2, 3 from the StageLin; B_f = [0, b],
-// b = (0, 0, b2, b3)', so G_0 = (R^-1)[1][1] b b'.  Returns the number of doublings, or 0 if they did not settle
-// (a non-finite value, or no settling within kSdaMaxSteps): the caller then runs the reference's fixed point.
-__device__ int dare_sda(double h, const double* a2, const double* a3, double b2, double b3, const M44& Q, const M22& R,
-                        double* P) {
-    double A[16] = {1.0, 0.0, h, 0.0, 0.0, 1.0, 0.0, h, a2[0], a2[1], a2[2], a2[3], a3[0], a3[1], a3[2], a3[3]};
-    const double r11 = R.v[0] / (R.v[0] * R.v[3] - R.v[1] * R.v[2]);      // (R^-1)[1][1]
-    const double bv[4] = {0.0, 0.0, b2, b3};
-    double G[16], H[16], M[16], W[16], WA[16], WG[16], T[16], U[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) G[4 * i + j] = r11 * bv[i] * bv[j];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) H[k] = Q.v[k];
+// The pad's P_inf by doubling; sm = this group's 8 x 16 doubles of LDS.  Returns the number of doublings with this
+// lane's entry of P in *P, or 0 if they did not settle (a zero / non-finite pivot, a non-finite H, no settling within
+// kSdaMaxSteps): the caller then runs the reference's fixed point.  Every lane of the wavefront must call it.
+__device__ int dare_sda16(double h, const StageLin& pad, const M44& Q, const M22& R, int i, int j, double* sm,
+                          double* P) {
+    double* sA = sm;        double* sG = sm + 16;  double* sH = sm + 32;  double* sM = sm + 48;
+    double* sV = sm + 64;   double* sW = sm + 80;  double* sT = sm + 96;  double* sU = sm + 112;
+    const int l = 4 * i + j;
+    // A_f: rows 0, 1 = [1 0 h 0], [0 1 0 h]; rows 2, 3 the StageLin's.  G_0 = (R^-1)[1][1] b b', b = (0, 0, b2, b3)'
+    double a = i == 0 ? (j == 0 ? 1.0 : (j == 2 ? h : 0.0)) : i == 1 ? (j == 1 ? 1.0 : (j == 3 ? h : 0.0))
+                                                            : (i == 2 ? pad.a2[j] : pad.a3[j]);
+    const double r11 = R.v[0] / (R.v[0] * R.v[3] - R.v[1] * R.v[2]);
+    const double bi = i == 2 ? pad.b2 : (i == 3 ? pad.b3 : 0.0), bj = j == 2 ? pad.b2 : (j == 3 ? pad.b3 : 0.0);
+    double g = r11 * bi * bj, hh = Q.v[l];
     for (int step = 1; step <= kSdaMaxSteps; ++step) {
-        mm44(G, H, M);
+        sA[l] = a; sG[l] = g; sH[l] = hh;
+        wave_lds_order();
+        double m = dot_xy(sG, sH, i, j) + (i == j ? 1.0 : 0.0);        // I + G H
+        double v = i == j ? 1.0 : 0.0;                                  // its inverse, built alongside
+        bool ok = true;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) M[5 * i] += 1.0;
-        if (!inv44(M, W)) return 0;
-        mm44(W, A, WA);
-        mm44(W, G, WG);
-        mm44(A, WG, T);                          // A W G
-        mm44_bt(T, A, U);                        // A W G A'
+        for (int c = 0; c < 4; ++c) {
+            wave_lds_order();                                           // earlier reads of sM / sV are done
+            sM[l] = m; sV[l] = v;
+            wave_lds_order();
+            int p = c;                                                  // the largest |M[r][c]|, r >= c
+            double best = fabs(sM[4 * c + c]);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) G[k] += U[k];
-        mm44(H, WA, T);                          // H W A
-        mm44_at(A, T, U);                        // A' H W A
-        double d = 0.0, hm = 0.0;
-        bool fin = true;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const double hn = H[k] + U[k];
-            d = fmax(d, fabs(hn - H[k]));
-            hm = fmax(hm, fabs(hn));
-            fin &= fabs(hn) <= 1.7976931348623157e308;
-            H[k] = hn;
+            for (int r = c + 1; r < 4; ++r) {
+                const double t = fabs(sM[4 * r + c]);
+                p = t > best ? r : p;
+                best = t > best ? t : best;
+            }
+            const int row = i == c ? p : (i == p ? c : i);            // this lane's row after swapping rows c, p
+            const double piv = sM[4 * p + c];
+            ok &= (piv != 0.0) & (fabs(piv) <= 1.7976931348623157e308);
+            const double ip = 1.0 / piv;
+            const double mm = sM[4 * row + j], vv = sV[4 * row + j];
+            const double f = sM[4 * row + c];
+            const double mc = sM[4 * p + j] * ip, vc = sV[4 * p + j] * ip;
+            m = i == c ? mc : fma(-f, mc, mm);
+            v = i == c ? vc : fma(-f, vc, vv);
         }
-        mm44(A, WA, T);                          // A W A
-#pragma unroll
-        for (int k = 0; k < 16; ++k) A[k] = T[k];
-        if (!fin) return 0;
+        wave_lds_order();
+        sW[l] = v;
+        wave_lds_order();
+        const double wa = dot_xy(sW, sA, i, j), wg = dot_xy(sW, sG, i, j);
+        sM[l] = wa; sV[l] = wg;                                         // W A, W G
+        wave_lds_order();
+        const double awg = dot_xy(sA, sV, i, j), hwa = dot_xy(sH, sM, i, j), awa = dot_xy(sA, sM, i, j);
+        sT[l] = awg; sU[l] = hwa;
+        wave_lds_order();
+        const double gn = g + dot_xyt(sT, sA, i, j);                   // G + A W G A'
+        const double hn = hh + dot_xty(sA, sU, i, j);                  // H + A' H W A
+        const bool bad = !ok || !(fabs(hn) <= 1.7976931348623157e308);
+        const double d = grp16_max(fabs(hn - hh)), hm = grp16_max(fabs(hn));
+        a = awa; g = gn; hh = hn;
+        if (__any(bad)) return 0;
         if (d <= 1e-15 * hm) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) P[k] = H[k];
+            *P = hh;
             return step;
         }
+        wave_lds_order();                                               // reads of this step before the next writes
     }
     return 0;
 }
 
 // Workgroup = 4 windows (16 lanes each).  1) every stage the 4 windows use, discretised, into LDS (one lane per
-// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by doubling (dare_sda; the
+// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by doubling (dare_sda16; the
 // reference's fixed point if it does not settle), in every workgroup (the same bits everywhere: no grid-wide
 // dependency);  3) each window's recursion from P = P_inf over stages
 // w+L-2 .. w;  its first gain is the QP's solution u0 = K x0 at control step w.
@@ -414,25 +387,14 @@ __global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restric
         }
     }
     __syncthreads();
-    // compute_P_inf on the pad stage: by doubling on lane 0 (dare_sda), the same bits in every workgroup
-    __shared__ double sP[16];
-    __shared__ int s_sda;
-    if (ln == 0) {
-        double Pd[16];
-        const int steps = dare_sda(m.h, pad.a2, pad.a3, pad.b2, pad.b3, Q, R, Pd);
-        s_sda = steps;
-        if (steps > 0) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) sP[k] = Pd[k];
-        }
-    }
-    __syncthreads();
+    // compute_P_inf on the pad stage: by doubling on every 16-lane group (dare_sda16), the same bits everywhere
+    __shared__ double sm[4][128];
     const MapLane c = map_lane(i, j, m.h, Q, R);
     double P, K0j, K1j;
+    const int steps = dare_sda16(m.h, pad, Q, R, i, j, sm[g], &P);
     int it;                                               // doublings (> 0), or -(fixed-point iterations)
-    if (s_sda > 0) {
-        P = sP[4 * i + j];
-        it = s_sda;
+    if (steps > 0) {
+        it = steps;
     } else {   // the doubling did not settle (not a stabilisable pad): the reference's fixed point, from P = Q
         const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2,
                      fb3 = pad.b3;

@@ -58,8 +58,9 @@ def test_cfg4_global_batch_on_one_gpu():
     schedule), solved to convergence on one GPU, checked through size-independent properties: every lane
     converges; lanes 0..4095 (make_x0 draws the same rows for any batch size) are bit for bit the cfg 2 solve of
     those 4,096 lanes (persistent schedule: per-lane results do not depend on the batch, its size or the
-    schedule); 64 lanes spread over the batch match the C oracle's decisions and trajectories; lane 0 the
-    reference's npz."""
+    schedule); the first 262,144 lanes (bench.make_x0 draws them as the cfg 3 batch) take exactly the C oracle's
+    decisions and its final costs within 1e-11, lane by lane (tests/golden/headline_oracle.npz); 1,024 lanes spread
+    over the whole batch match the live C oracle's decisions and trajectories; lane 0 the reference's npz."""
     import torch
     from bench import load_refs, make_x0
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
@@ -76,6 +77,15 @@ def test_cfg4_global_batch_on_one_gpu():
     st = r.status.cpu().numpy()
     assert (st == 1).all(), np.bincount(st)
     ni = r.n_iter.cpu().numpy()
+    nr, cost = r.n_rollouts.cpu().numpy(), r.cost.cpu().numpy()
+    fx = load_golden("headline_oracle")
+    L = len(fx["n_iter"])
+    np.testing.assert_array_equal(make_x0(L), x0[:L])
+    np.testing.assert_array_equal(ni[:L], fx["n_iter"])
+    np.testing.assert_array_equal(st[:L], fx["status"])
+    np.testing.assert_array_equal(nr[:L], fx["n_rollouts"])
+    rel = np.abs(cost[:L] - fx["cost"]) / np.abs(fx["cost"])
+    assert rel.max() < 1e-11, rel.max()
     head = {k: getattr(r, k)[:4096].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")}
     head["n_iter"], head["n_roll"] = ni[:4096], r.n_rollouts[:4096].cpu().numpy()
     pick = np.linspace(0, B - 1, 1024).astype(np.int64)   # ~3 s of the C oracle on the box's host cores

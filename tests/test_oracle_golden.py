@@ -4,6 +4,8 @@ Golden sources:
   * task2_reference_output.npz -- the reference's own committed output (main.task_2);
   * the other fixtures -- produced by running the reference itself (tests/golden/make_golden.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -216,3 +218,26 @@ def test_c_oracle_stress_lanes_vs_reference(golden, task2_refs):
             assert (no, int(o["status"][j]), int(o["n_rollouts"][j])) == \
                 (nr, int(g["status"][j]), int(g["n_rollouts"][j])), int(lane)
     assert n_tie_free >= 4          # the converged lanes
+
+
+@pytest.mark.parametrize("name,spread", [("headline_oracle", 0.5), ("stress_oracle", 1.5)])
+def test_batch_fixtures_reproduce_on_the_c_oracle(golden, name, spread):
+    """The whole-batch fixtures (tests/golden/make_headline_oracle.py, make_stress_oracle.py: the C oracle over
+    bench.py's 262,144-lane cfg 3 and stress workloads) are the C oracle's own outcome: 64 lanes spread over the
+    batch, re-solved here, give the stored decisions and costs exactly; the workload's shape is the bench's."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import load_refs, make_x0
+    from oracle import c_oracle
+    g = golden(name)
+    B = len(g["n_iter"])
+    assert B == 262144 and float(g.get("spread", spread)) == spread and int(g["max_iters"]) == 5000
+    xr, ur = load_refs()
+    pick = np.linspace(0, B - 1, 64).astype(np.int64)
+    pick = pick[g["n_iter"][pick] < 1000]                  # keep the check to seconds
+    o = c_oracle.newton_solve(make_x0(B, spread=spread)[pick], xr, ur, max_iters=5000, tol=1e-4, beta=0.7, c=0.5,
+                              gamma_0=0.1, max_ls=20)
+    np.testing.assert_array_equal(o["n_iter"], g["n_iter"][pick])
+    np.testing.assert_array_equal(o["status"], g["status"][pick])
+    np.testing.assert_array_equal(o["n_rollouts"], g["n_rollouts"][pick])
+    np.testing.assert_array_equal(o["cost"], g["cost"][pick])
