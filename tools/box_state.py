@@ -119,8 +119,8 @@ class Sampler:
     """Background sysfs sampler.  ``mark()`` starts a window; ``window()`` returns {channel: [mean, min, max]} over the
     samples since the last mark (plus the sample count and the window's seconds)."""
 
-    def __init__(self, device_index: int = 0, period: float = 0.1):
-        dev = pci_dir(device_index)
+    def __init__(self, device_index: int = 0, period: float = 0.1, dev: str | None = None):
+        dev = dev or pci_dir(device_index)
         self.dev = dev
         self.ch = _Channels(dev) if dev else None
         self.period = period
