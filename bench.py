@@ -335,7 +335,7 @@ class BoxMonitor:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import box_state
         self._bs = box_state
-        self.use_smi = use_smi          # amd-smi's first GPU is this process's only on a one-GPU box
+        self.use_smi = use_smi          # amd-smi's GPU matched by PCI address (tools/box_state.smi_index)
         self.s = box_state.Sampler(device_index, 0.1).start()
 
     def mark(self):
@@ -345,7 +345,8 @@ class BoxMonitor:
         return self.s.window()
 
     def smi(self):
-        return self._bs.smi_counters(20.0) if self.use_smi else {}
+        bdf = os.path.basename(self.s.dev) if self.s.dev else None
+        return self._bs.smi_counters(20.0, bdf) if self.use_smi else {}
 
     def summary(self, win, smi0, smi1) -> dict:
         out = {self.KEYS[k]: v for k, v in win.items() if k in self.KEYS}
@@ -556,7 +557,7 @@ def main():
     strong = a.global_batch is not None
     total = a.global_batch if strong else a.batch * world
     eng = AcrobotEngine()
-    box = None if a.no_box or rank != 0 else BoxMonitor(gd.local_device_index(local_rank), use_smi=world == 1)
+    box = None if a.no_box or rank != 0 else BoxMonitor(gd.local_device_index(local_rank))
     main_leg = NewtonLeg(a, gd, eng, x_ref, u_ref, total, not a.no_timing,
                          u0_zero=False if a.u0_zero == "off" else None).run(a.steps, a.warmup, box)
     res = main_leg.res

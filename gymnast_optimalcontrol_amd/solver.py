@@ -86,6 +86,12 @@ class BatchedNewtonSolver:
     # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
     # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.
     TAIL_LANES_PER_CU = 4
+    # Placement selection (select_placement): the phase kernel's speed depends on where its six stream buffers land
+    # (one box: 1.92-2.06 ms per launch for six allocations alive at once, each stable for its lifetime;
+    # profiles/r05/placement/), so a large pipelined solver allocates up to this many stream sets, times a short
+    # probe of the real phase kernel on each and keeps the fastest (the same bits whichever it keeps).
+    PLACEMENT_TRIALS = 1      # 3 once validated on the GPU (see select_placement)
+    PLACEMENT_PROBE_ITERS = 24
     # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
     # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
     CAND_SLOTS = 32768
@@ -106,7 +112,8 @@ class BatchedNewtonSolver:
                  chunk: int = 128, reorder: bool = True, schedule_lanes: int | None = None,
                  capture_lanes=None, capture_every: int = 1, split_waves: bool = True,
                  capture_sigma=(0, 1, 2), tail_lanes: int | None = None, tail_chunk: int = 128,
-                 compact: bool | None = None, world_size: int = 1, cand_slots: int | None = None):
+                 compact: bool | None = None, world_size: int = 1, cand_slots: int | None = None,
+                 arena=False, placement_trials: int | None = None):
         if B <= 0:
             raise ValueError("batch must hold at least one lane")
         # the automatic schedule choice is made on ``schedule_lanes`` (default: this batch).  Sharded solves pass
@@ -139,10 +146,21 @@ class BatchedNewtonSolver:
         dev = engine.device
         e = lambda *s, dt=F64: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
         Bp, N, T = self.Bp, self.N, self.T
-        self.x = [e(N, 2, Bp, 2), e(N, 2, Bp, 2)]
-        self.u = [e(T, 2, Bp, 1), e(T, 2, Bp, 1)]      # control planes (tau1, tau2)
-        self.K1 = e(T, 2, Bp, 2)                       # gain row 1, pairs
-        self.cs = e(T, 2, Bp, 1)                       # planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1
+        shapes = [(N, 2, Bp, 2), (N, 2, Bp, 2), (T, 2, Bp, 1), (T, 2, Bp, 1), (T, 2, Bp, 2), (T, 2, Bp, 1)]
+        if arena is not False and arena is not None:
+            # the six streams carved from one allocation, each 2 MiB aligned, in this order (arena: True = a torch
+            # allocation, or a callable n -> fp64 device tensor of n elements that provides it)
+            al = (2 << 20) // 8
+            offs, n = [], 0
+            for sh in shapes:
+                offs.append(n)
+                n += -(-int(np.prod(sh)) // al) * al
+            self._arena = arena(n) if callable(arena) else e(n)
+            st = [self._arena[o:o + int(np.prod(sh))].view(sh) for o, sh in zip(offs, shapes)]
+        else:
+            st = [e(*sh) for sh in shapes]
+        self._stream_shapes = shapes
+        self._set_streams(st)
         self.cost, self.dJ, self.smax, self.gamma = e(Bp), e(Bp), e(Bp), e(Bp)
         i32 = torch.int32
         self.status, self.n_iter, self.res_buf, self.n_roll = (e(Bp, dt=i32) for _ in range(4))
@@ -187,9 +205,7 @@ class BatchedNewtonSolver:
         self.split_waves = bool(split_waves)
         b.flags = ((_lib.FLAG_U0_ZERO if self.u0_zero else 0) | (_lib.FLAG_X_CKPT if self.checkpoint else 0) |
                    (0 if self.split_waves else _lib.FLAG_RUN_SINGLE) | (_lib.FLAG_REF_LANE if self.ref_lane else 0))
-        b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
-        b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
-        for name in ("K1", "cs", "cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
+        for name in ("cost", "dJ", "smax", "gamma", "status", "n_iter", "res_buf", "n_roll",
                      "retry_list", "counters", "cand_ok", "partials", "stats"):
             setattr(b, name, getattr(self, name).data_ptr())
         if self.ref_lane:
@@ -199,6 +215,7 @@ class BatchedNewtonSolver:
         b.hist_cost = _lib.ptr(self.hist_cost)
         b.hist_smax = _lib.ptr(self.hist_smax)
         self.batch = b
+        self._set_streams(st)
         self.k = 0
         self.timeline = None     # diagnostics: a list records (iterations, active lanes, host time) per sync
         self.timing = None
@@ -275,6 +292,76 @@ class BatchedNewtonSolver:
         self._cap_pos = None
         self._cap_log = []
         self._sig_log = []
+        self.placement = None
+        if placement_trials is None:
+            placement_trials = (self.PLACEMENT_TRIALS if (auto_schedule and self.pipeline and not self.persistent and
+                                                          arena is False) else 1)
+        if int(placement_trials) > 1:
+            self.select_placement(int(placement_trials))
+
+    def _set_streams(self, st):
+        """Use the stream set st = [x0, x1, u0, u1, K1, cs] (K1 and cs zeroed, as at construction)."""
+        self.x = list(st[0:2])
+        self.u = list(st[2:4])                         # control planes (tau1, tau2)
+        self.K1 = st[4]                                # gain row 1, pairs
+        self.cs = st[5]                                # planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1
+        self.K1.zero_(); self.cs.zero_()
+        b = getattr(self, "batch", None)
+        if b is not None:
+            b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
+            b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
+            b.K1, b.cs = self.K1.data_ptr(), self.cs.data_ptr()
+
+    def select_placement(self, trials: int, iters: int | None = None) -> dict:
+        """Keep the fastest of up to ``trials`` stream-buffer placements.  The pipelined phase kernel moves its bytes at
+        a speed that depends on where its six streams land in HBM (one box, six allocations alive at once: 1.92 to
+        2.06 ms per launch, each stable over its lifetime; profiles/r05/placement/).  This allocates further stream
+        sets while the free memory allows (beside the lane-major results a solve allocates), runs ``iters``
+        iterations of the real schedule on a synthetic headline-like batch on each, timed with HIP events on the
+        solver's stream, keeps the fastest and releases the others.  Setup only: solve() re-initialises every buffer,
+        and every placement computes the same bits.  Records {"probe_ms": [...], "chosen": i} in ``self.placement``."""
+        iters = int(iters or self.PLACEMENT_PROBE_ITERS)
+        dev = self.eng.device
+        e = lambda sh: torch.empty(sh, dtype=F64, device=dev)  # noqa: E731
+        set_bytes = 8 * sum(int(np.prod(sh)) for sh in self._stream_shapes)
+        B, N, T = self.B, self.N, self.T
+        results_bytes = 8 * B * (4 * N + 2 * T + 8 * T + 2 * T)      # finalize's x, u, K, sigma
+        free, _ = torch.cuda.mem_get_info(dev)
+        k = min(int(trials), 1 + max(0, int((free - results_bytes - (4 << 30)) // max(set_bytes, 1))))
+        if k < 2:
+            return {}
+        sets = [[*self.x, *self.u, self.K1, self.cs]] + [[e(sh) for sh in self._stream_shapes] for _ in range(k - 1)]
+        # a deterministic headline-like batch: th1, th2 spread over (-0.5, 0.5), at rest
+        lane = torch.arange(self.B, device=dev, dtype=F64)
+        x0 = torch.zeros((self.B, 4), dtype=F64, device=dev)
+        x0[:, 0] = torch.frac(lane * 0.6180339887498949) - 0.5
+        x0[:, 1] = torch.frac(lane * 0.7548776662466927) - 0.5
+        saved_launches = dict(self.launches)
+        times = []
+        for st in sets:
+            self._set_streams(st)
+            self.max_iters = iters + 1
+            self.init(x0)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(iters):
+                self.iteration()
+            ev[1].record()
+            torch.cuda.synchronize(dev)
+            times.append(ev[0].elapsed_time(ev[1]) / iters)
+        best = int(np.argmin(times))
+        self._set_streams(sets[best])
+        sets = None
+        self.max_iters = None
+        self.k = 0
+        self.launches = saved_launches
+        if self.timing is not None:
+            self.reset_timing()
+        for t in (self.hist_cost, self.hist_smax):
+            if t is not None:
+                t.fill_(float("nan"))
+        self.placement = {"trials": k, "probe_ms_per_iteration": times, "chosen": best}
+        return self.placement
 
     def ensure_cand_scratch(self) -> bool:
         """Allocate the candidate scratch (cand_slots slots, ~24 KiB each at T = 500) if this solver uses one and has

@@ -82,16 +82,51 @@ class _Channels:
         return out
 
 
-def smi_counters(timeout: float = 30.0) -> dict:
-    """amd-smi's accumulated throttle and energy counters of the first GPU it lists (the box's one GPU), or {}:
-    ``acc`` (the SMU's accumulation ticks), ``ppt`` / ``socket_thermal`` / ``hbm_thermal`` / ``prochot`` (ticks spent
-    under that limit) and ``energy_j``.  Two snapshots give the share of a window spent at the power cap and the
-    energy it used."""
+def _smi_json(args, timeout):
     import json
     import subprocess
+    out = subprocess.run(["amd-smi", *args, "--json"], capture_output=True, text=True, timeout=timeout).stdout
+    i = min(k for k in (out.find("{"), out.find("[")) if k >= 0)
+    return json.loads(out[i:])
+
+
+_SMI_INDEX = {}
+
+
+def smi_index(bdf: str | None, timeout: float = 30.0) -> int | None:
+    """amd-smi's index of the GPU at PCI address ``bdf`` (e.g. 0000:0d:00.0, from pci_dir), from ``amd-smi list``;
+    with one GPU listed, that one; None if it cannot be told."""
+    if bdf in _SMI_INDEX:
+        return _SMI_INDEX[bdf]
+    idx = None
     try:
-        out = subprocess.run(["amd-smi", "metric", "--json"], capture_output=True, text=True, timeout=timeout).stdout
-        g = json.loads(out[out.index("{"):])["gpu_data"][0]
+        lst = _smi_json(["list"], timeout)
+        lst = lst if isinstance(lst, list) else lst.get("gpu_list", lst.get("gpus", []))
+        for e in lst:
+            if bdf and str(e.get("bdf", "")).lower() == bdf.lower():
+                idx = int(e["gpu"])
+        if idx is None and len(lst) == 1:
+            idx = int(lst[0].get("gpu", 0))
+    except Exception:
+        idx = None
+    _SMI_INDEX[bdf] = idx
+    return idx
+
+
+def smi_counters(timeout: float = 30.0, bdf: str | None = None) -> dict:
+    """amd-smi's accumulated throttle and energy counters of the GPU at ``bdf`` (the one GPU listed, if bdf is None),
+    or {}: ``acc`` (the SMU's accumulation ticks), ``ppt`` / ``socket_thermal`` / ``hbm_thermal`` / ``prochot``
+    (ticks spent under that limit) and ``energy_j``.  Two snapshots give the share of a window spent at the power
+    cap and the energy it used."""
+    try:
+        idx = smi_index(bdf, timeout)
+        if idx is None:
+            return {}
+        data = _smi_json(["metric", "-g", str(idx)], timeout)
+        gl = data["gpu_data"] if isinstance(data, dict) else data
+        g = next((e for e in gl if int(e.get("gpu", idx)) == idx), None) if len(gl) != 1 else gl[0]
+        if g is None:
+            return {}
         th = g.get("throttle", {})
         rec = {"acc": th.get("accumulation_counter"), "ppt": th.get("ppt_accumulated"),
                "socket_thermal": th.get("socket_thermal_accumulated"), "hbm_thermal": th.get("hbm_thermal_accumulated"),

@@ -36,12 +36,13 @@ def main():
     lib.pp_valu.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_double, C.c_void_p]
     stream = torch.cuda.current_stream().cuda_stream
     samp = Sampler(0, 0.05).start()
+    bdf = os.path.basename(samp.dev) if samp.dev else None
     B, T = 262144, 500
     out = {"lanes": B, "stages": T}
 
     def window(run, seconds):
         torch.cuda.synchronize()
-        s0 = smi_counters()
+        s0 = smi_counters(bdf=bdf)
         samp.mark()
         t0 = time.perf_counter()
         n = 0
@@ -53,7 +54,7 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         w = samp.window()
-        d = smi_delta(s0, smi_counters())
+        d = smi_delta(s0, smi_counters(bdf=bdf))
         return n, dt, w, d
 
     samp.mark()
@@ -115,6 +116,26 @@ def main():
                        "smi": d, "uj_per_lane_it": 1e6 * p / rate, "uj_per_lane_it_dynamic": 1e6 * (p - p_idle) / rate,
                        "bytes_per_lane_it": 80096, "valu_wave_instr_per_lane_it": 724082227.2 * 809 / 102862555}
     print("headline", json.dumps(out["headline"]), flush=True)
+    leg.free()
+    # the general path (tau1 planes streamed: 92,096 B per lane-iteration) on the same box
+    legg = bench.NewtonLeg(ns, gd, AcrobotEngine(), x_ref, u_ref, B, False, u0_zero=False)
+    legg.solver.solve(legg.x0_dev, 5000, sync_every=4)
+    its[0] = 0
+
+    def solve_g():
+        r = legg.solver.solve(legg.x0_dev, 5000, sync_every=4)
+        its[0] += r.lane_iterations
+    n, dt, w, d = window(solve_g, max(a.seconds, 3.5))
+    rate = its[0] / dt
+    p = w.get("power_ppt_in_w", [0.0])[0]
+    out["general"] = {"lane_it_per_s": rate, "power_w": w.get("power_ppt_in_w"), "sclk_mhz": w.get("dpm_sclk_mhz"),
+                      "smi": d, "uj_per_lane_it": 1e6 * p / rate, "uj_per_lane_it_dynamic": 1e6 * (p - p_idle) / rate,
+                      "bytes_per_lane_it": 92096}
+    for k, b in (("headline", 80096), ("general", 92096)):     # whole-solve bytes/s (launch gaps included)
+        out[k]["solve_GBs"] = out[k]["lane_it_per_s"] * b / 1e9
+    print("general", json.dumps(out["general"]), flush=True)
+    print("solve GB/s: stream probe %.0f, headline %.0f, general %.0f" % (out["stream"]["GBs"],
+          out["headline"]["solve_GBs"], out["general"]["solve_GBs"]), flush=True)
     samp.stop()
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     json.dump(out, open(a.out, "w"), indent=1)
