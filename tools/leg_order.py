@@ -100,6 +100,8 @@ def main():
         kw = {"checkpoint": True} if name == "cfg3ck" else {"arena": True} if name == "cfg3arena" else {}
         if name == "cfg3contig":
             kw = {"arena": contig_arena}
+        if name == "cfg3sel":
+            kw = {"placement_trials": 3}
         ns.schedule = "serial" if name.endswith("ser") else "auto"
         leg = bench.NewtonLeg(ns, gd, eng, x_ref, u_ref, total, True,
                               u0_zero=False if name.startswith("general") else None, spread=spread, **kw)
@@ -109,7 +111,8 @@ def main():
                                                    ("K1", sv.K1), ("cs", sv.cs))}
         if sv._cand_scratch is not None:
             ptrs["cand"] = hex(sv._cand_scratch.data_ptr())
-        print(name, "buffers", ptrs, "built in", round(time.perf_counter() - t_build, 2), "s", flush=True)
+        print(name, "buffers", ptrs, "built in", round(time.perf_counter() - t_build, 2), "s", "placement",
+              sv.placement, flush=True)
         res = None
         t_smi = time.perf_counter()
         smi0 = smi_counters(bdf=os.path.basename(samp.dev) if samp.dev else None)
