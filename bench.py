@@ -633,6 +633,11 @@ def main():
         out["roofline"].update({k: v for k, v in roof.items() if k not in out["roofline"]})
         out["kernels"] = kern
     out["schedule"] = main_leg.schedule()
+    if main_leg.solver.placement:
+        # the stream-buffer placement the solver picked (BatchedNewtonSolver.select_placement)
+        out["placement"] = dict(main_leg.solver.placement, note=(
+            "stream-buffer sets probed at construction (24 iterations of the real schedule each, two rounds, ms per "
+            "iteration) and the one kept; outside the timed region"))
     if world > 1:
         # per-rank diagnostics of the main leg: a sub-linear scaling curve then says whether stragglers (spread of
         # the ranks' own elapsed times and lane-iterations), the statistics all-reduce or its read-back is the cause
