@@ -673,3 +673,26 @@ def test_per_lane_references(golden, task2_refs):
         BatchedNewtonSolver(eng, XR, UR, B, checkpoint=True, **kw)
     with pytest.raises(ValueError):
         BatchedNewtonSolver(eng, XR[:10], UR[:10], B, **kw)
+
+
+def test_placement_selection_is_invisible(task2_refs):
+    """BatchedNewtonSolver.select_placement (round 5: up to three stream-buffer sets, a short probe of the real schedule
+    on each, the fastest kept) changes where the streams live, not what they compute: the solve after selection is
+    bit for bit the solve of a solver that kept its first allocation, on a batch with backtracking, LS-failure and
+    NaN lanes and per-lane histories (which the probe must not leave behind)."""
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    B, H = 2000, 120
+    x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
+    x0[11] = np.nan
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, pipeline=True, hist_len=H)
+    a = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=1, **kw)
+    s = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=3, **kw)
+    assert a.placement is None and s.placement["trials"] >= 2 and 0 <= s.placement["chosen"] < s.placement["trials"]
+    assert s.x[0].data_ptr() == s.batch.x[0] and s.K1.data_ptr() == s.batch.K1 and s.cs.data_ptr() == s.batch.cs
+    ra, rs = a.solve(x0, H), s.solve(x0, H)
+    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax"):
+        assert np.array_equal(getattr(ra, name).cpu().numpy(), getattr(rs, name).cpu().numpy(), equal_nan=True), name
+    assert (ra.n_rollouts > ra.n_iter).sum().item() > 10 and (ra.status == 2).sum().item() > 0
