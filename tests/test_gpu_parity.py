@@ -687,7 +687,7 @@ def test_placement_selection_is_invisible(task2_refs):
     x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
     x0[11] = np.nan
     eng = AcrobotEngine()
-    kw = dict(tol=1e-4, gamma_0=0.1, pipeline=True, hist_len=H)
+    kw = dict(tol=1e-4, gamma_0=1.0, pipeline=True, hist_len=H)     # gamma_0 = 1: wide starts backtrack early
     a = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=1, **kw)
     s = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=3, **kw)
     assert a.placement is None and s.placement["trials"] >= 2 and 0 <= s.placement["chosen"] < s.placement["trials"]
