@@ -626,6 +626,11 @@ def main():
             # the PMC pass profiles one 20-iteration launch; a bench launch runs up to `chunk` iterations
             traffic = ratio * roof["algorithmic_bytes_per_launch"]
             src = (src or "") + "; measured / algorithmic ratio of a 20-iteration launch, scaled to this launch"
+        elif ratio is not None and roof.get("algorithmic_bytes_per_launch"):
+            # the PMC passes profile launches with every lane active; this run's average launch carries fewer lanes
+            # near the end of the solve, so its per-launch traffic is the measured ratio times its own bytes
+            traffic = ratio * roof["algorithmic_bytes_per_launch"]
+            src = (src or "") + "; measured / algorithmic ratio of full launches, times this run's bytes per launch"
         roof.update({"traffic": traffic, "traffic_over_algorithmic": ratio, "traffic_source": src,
                      "survey_bytes_per_iteration": algorithmic_bytes(N)["survey_per_iteration"], "fp64_valu": valu})
         # the ordering the contract prescribes: bound, achieved, peak, unit, frac, traffic first
