@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--max-iters", type=int, default=5000)
     ap.add_argument("--spread", type=float, default=0.5, help="th0 ~ U(+-spread) (1.5: the stress workload)")
     ap.add_argument("--sync-every", type=int, default=4, help="host synchronisation cadence (bench.py's default)")
+    ap.add_argument("--box", action="store_true", help="record SCLK / power over each solve (sysfs)")
     a = ap.parse_args()
     import torch
     from bench import load_refs, make_x0
@@ -49,7 +50,12 @@ def main():
     default_u0z = s.u0_zero
     xd = eng.t(x0)
     libs = {p: _lib.load(split(p)[0]) for p in a.libs}
-    res = {p: {"bwd": [], "trial": [], "its": [], "sec": []} for p in a.libs}
+    res = {p: {"bwd": [], "trial": [], "its": [], "sec": [], "sclk": [], "power": []} for p in a.libs}
+    samp = None
+    if a.box:   # sysfs clocks / power over each solve (tools/box_state.py)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from box_state import Sampler
+        samp = Sampler(0, 0.05).start()
     for r in range(a.rounds + 1):
         for p in a.libs:
             eng.lib = libs[p]
@@ -62,7 +68,15 @@ def main():
             s.batch.flags = (_lib.FLAG_U0_ZERO if s.u0_zero else 0) | (_lib.FLAG_X_CKPT if s.checkpoint else 0)
             s.reset_timing()
             s.batch.timing = None if notime else C.pointer(s.timing)
+            if samp is not None:
+                torch.cuda.synchronize()
+                samp.mark()
             out = s.solve(xd, a.max_iters, sync_every=a.sync_every)
+            if samp is not None:
+                torch.cuda.synchronize()
+                w = samp.window()
+                res[p]["sclk"].append(w.get("dpm_sclk_mhz", [float("nan")])[0])
+                res[p]["power"].append(w.get("power_ppt_in_w", [float("nan")])[0])
             kt = s.kernel_times()
             if notime:
                 kt = {k: (0.0, 0) for k in kt}
@@ -86,6 +100,7 @@ def main():
         d = res[p]
         print(json.dumps({"lib": os.path.basename(p), "bwd_ms": float(np.median(d["bwd"])),
                           "trial_ms": float(np.median(d["trial"])), "Mits": float(np.median(d["its"])) / 1e6,
+                          "sclk_mhz": [round(v) for v in d["sclk"]], "power_w": [round(v) for v in d["power"]],
                           "bwd_all": [round(v, 4) for v in d["bwd"]], "trial_all": [round(v, 4) for v in d["trial"]]}),
               flush=True)
 
