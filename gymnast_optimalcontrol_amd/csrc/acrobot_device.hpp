@@ -106,16 +106,23 @@ __device__ __forceinline__ void fast_sincos(double x, double* s, double* c, cons
     constexpr double kPio2Hi = 1.57079632679489655800e+00;   // 0x3FF921FB54442D18
     constexpr double kPio2Lo = 6.12323399573676603587e-17;   // 0x3C91A62633145C07
     const double kq = __builtin_rint(x * kTwoOverPi);
-    const double qn = (fabs(kq) < 1048576.0) ? kq : __builtin_nan("");   // outside the domain: NaN
+    // outside the domain: NaN, by replacing the high word only (kq's bits otherwise: one select, not two)
+    const uint64_t kb = __builtin_bit_cast(uint64_t, kq);
+    const uint32_t qh = (fabs(kq) < 1048576.0) ? (uint32_t)(kb >> 32) : 0x7FF80000u;
+    const double qn = __builtin_bit_cast(double, ((uint64_t)qh << 32) | (kb & 0xFFFFFFFFull));
     const double r = fma(-qn, kPio2Lo, fma(-qn, kPio2Hi, x));
     const double z = r * r;
     const double sr = ksin<V3>(r, z, k);
     const double cr = kcos<V3>(z, k);
-    const int q = (int)qn;                 // v_cvt_i32_f64 maps NaN to 0
+    const uint32_t q = (uint32_t)(int)qn;  // v_cvt_i32_f64 maps NaN to 0
     const double ss = (q & 1) ? cr : sr;   // quadrant rotation
     const double cc = (q & 1) ? sr : cr;
-    *s = (q & 2) ? -ss : ss;
-    *c = ((q + 1) & 2) ? -cc : cc;
+    // signs: quadrant bit 1 of q (of q + 1 for the cosine) moved to the sign bit and xor'ed in, which is negation
+    // bit for bit (NaN included), without a compare and a select
+    const uint64_t ns = (uint64_t)((q << 30) & 0x80000000u) << 32;
+    const uint64_t nc = (uint64_t)(((q + 1u) << 30) & 0x80000000u) << 32;
+    *s = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, ss) ^ ns);
+    *c = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, cc) ^ nc);
 }
 
 // 1/v for v in the well-conditioned range of det M: hardware reciprocal + two Newton steps.

@@ -360,7 +360,7 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
     prio_start<BAND ? 1 : PRIO_NONE>();
     for (int t = 0; t < T; ++t) {
         const TrialStage q = pre;
-        if (t + 1 < T) fetch(pre, t + 1);
+        fetch(pre, t + 1 < T ? t + 1 : t);   // unconditional (the last stage's copy unused): no phi, no copies
         body(q, t);
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
@@ -623,9 +623,10 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
         prio_band<BAND ? 0 : PRIO_NONE>(T - 1 - t, T);
         const double2 xa = pa, xb = pb;
         const double ut0 = pu0, ut1 = pu1;
-        if (t > 0) {
-            const auto rX = rsrc(Xb + (int64_t)(t - 1) * (2 * (int64_t)row));
-            const auto rU = rsrc(Ub + (int64_t)(t - 1) * row);
+        {   // unconditional (at t = 0 stage 0 again, unused): no phi, no copies of the prefetch registers
+            const int tp = __builtin_amdgcn_readfirstlane(t > 0 ? t - 1 : 0);   // wave-uniform
+            const auto rX = rsrc(Xb + (int64_t)tp * (2 * (int64_t)row));
+            const auto rU = rsrc(Ub + (int64_t)tp * row);
             pa = bld2(rX, o2, 0);
             pb = bld2(rX, o2, WROW);
             if (!U0Z) pu0 = bld1(rU, o1, 0);
