@@ -48,6 +48,37 @@ def test_point_primitives_vs_reference(eng, golden):
     np.testing.assert_allclose(B.cpu().numpy(), g["B_c"], rtol=1e-10, atol=1e-12)
 
 
+def test_trigonometry_quadrants_and_domain(eng):
+    """The device sin/cos (acrobot_device.hpp fast_sincos: Cody-Waite reduction, quadrant selects and sign bits)
+    through gym_continuous_dynamics against the NumPy oracle (libm sin / cos): every quadrant, both signs, -0,
+    angles at multiples of pi/2 and next to them, large arguments inside the domain; outside it (|th| * 2/pi >= 2^20,
+    inf, NaN) the accelerations are NaN, so such a lane's cost is NaN and Armijo fails as for any non-finite value."""
+    from oracle import acrobot_np as ref
+    k = np.arange(-24, 25)
+    base = np.concatenate([k * (np.pi / 2), k * (np.pi / 2) + 1e-9, k * (np.pi / 2) - 1e-9, k * 0.37 + 0.011,
+                           [0.0, -0.0, 1e-300, -1e-300, 3.0, -3.0]])
+    big = np.array([1e3, -1e3, 12345.678, -98765.4321, 1e5, -1e5, 1.6e6, -1.6e6])
+    rng = np.random.default_rng(5)
+    ang = np.concatenate([base, big])
+    n = len(ang)
+    X = np.stack([ang, rng.permutation(ang), rng.uniform(-3, 3, n), rng.uniform(-3, 3, n)], 1)
+    U = np.stack([np.zeros(n), rng.uniform(-2, 2, n)], 1)
+    got = eng.continuous_dynamics(X, U).cpu().numpy()
+    want = ref.continuous_dynamics(X, U)
+    small = (np.abs(X[:, 0]) < 100) & (np.abs(X[:, 1]) < 100)
+    np.testing.assert_allclose(got[small], want[small], rtol=1e-12, atol=1e-12)
+    # large in-domain arguments: the reduction's error grows with the quadrant count (2-term pi/2)
+    np.testing.assert_allclose(got[~small], want[~small], rtol=1e-8, atol=1e-8)
+    out = np.array([1.7e6, -1.7e6, 1e7, 1e300, np.inf, -np.inf, np.nan])
+    m = len(out)
+    Xo = np.stack([out, np.full(m, 0.3), np.zeros(m), np.zeros(m)], 1)
+    Xo2 = np.stack([np.full(m, 0.3), out, np.zeros(m), np.zeros(m)], 1)
+    Uo = np.zeros((m, 2))
+    for Xd in (Xo, Xo2):
+        g = eng.continuous_dynamics(Xd, Uo).cpu().numpy()
+        assert np.isnan(g[:, 2:]).all(), g
+
+
 def test_reference_style_point_calls(tg, golden):
     from gymnast_optimalcontrol_amd import dynamics as dyn
     g = golden("kat_primitives")
