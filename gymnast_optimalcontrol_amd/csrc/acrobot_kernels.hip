@@ -108,17 +108,7 @@ __device__ __forceinline__ void st_nt(double* p, double a) { __builtin_nontempor
 // VGPRs and the per-stage 64-bit address arithmetic.  Offsets stay below 2^31 (Bp <= GYM_MAX_BP).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-// gfx950 cache-policy bits: nt (streamed once).  GYM_STREAM_CP / GYM_STORE_CP override the solver streams' load and
-// store policy for the A/B measurement of tools/policy_ab.sh only (variant builds; the product uses nt for both)
-#ifndef GYM_STREAM_CP
-#define GYM_STREAM_CP 2
-#endif
-#ifndef GYM_STORE_CP
-#define GYM_STORE_CP -1
-#endif
-constexpr int kNT = GYM_STREAM_CP;
-template <int CP>
-__device__ constexpr int kStoreCP() { return GYM_STORE_CP < 0 ? CP : GYM_STORE_CP; }
+constexpr int kNT = 2;  // gfx950 cache-policy bits: nt (streamed once; other policies measured, profiles/r05/policy)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
@@ -132,13 +122,11 @@ __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, uint32_t vo, ui
 }
 template <int CP = kNT>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a, double b) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so,
-                                           kStoreCP<CP>());
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(a, b)), r, vo, so, CP);
 }
 template <int CP = kNT>
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, double a) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so,
-                                           kStoreCP<CP>());
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, vo, so, CP);
 }
 
 __device__ __forceinline__ void pin(double v) { asm volatile("" : : "v"(v)); }
