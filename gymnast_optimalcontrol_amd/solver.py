@@ -89,8 +89,10 @@ class BatchedNewtonSolver:
     # Placement selection (select_placement): the phase kernel's speed depends on where its six stream buffers land
     # (one box: 1.92-2.06 ms per launch for six allocations alive at once, each stable for its lifetime;
     # profiles/r05/placement/), so a large pipelined solver allocates up to this many stream sets, times a short
-    # probe of the real phase kernel on each and keeps the fastest (the same bits whichever it keeps).
-    PLACEMENT_TRIALS = 3
+    # probe of the real phase kernel on each and keeps the fastest (the same bits whichever it keeps).  Of the 12 sets
+    # probed in the round-5 final lines half were slow (4.10-4.40 ms per probe iteration against 3.95-4.01): four sets
+    # leave one selection in 16 on a slow placement, three one in 8 (profiles/r05/final*/bench.log "placement").
+    PLACEMENT_TRIALS = 4
     PLACEMENT_PROBE_ITERS = 24
     # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
     # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
