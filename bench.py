@@ -390,6 +390,26 @@ def stress_tail_record(leg, ks, T: int) -> dict:
     return rec
 
 
+def persistent_chain_record(leg, ks, T: int) -> dict:
+    """The bound of a latency-bound persistent leg (BASELINE cfg 2): k_nt_run2 runs every lane's iterations back to
+    back, so a launch lasts as long as its slowest lane's chain; the run kernel's seconds per solve over the longest
+    lane's iteration count are one lane-iteration's latency (a sweep pass and a trial pass, T stages each) and, at the
+    leg's SCLK, the cycles per stage of that chain.  share_of_solve = the run kernel's share of the
+    measured seconds per solve (the rest: init, statistics, host synchronisation, results)."""
+    steps = max(leg.steps, 1)
+    if not ks or "run" not in ks or not ks["run"]["launches"]:
+        return {}
+    run_s = ks["run"]["avg_ms"] * ks["run"]["launches"] / 1e3 / steps
+    n_max = int(leg.res.n_iter.max().item())
+    lat = run_s / max(n_max, 1)
+    rec = {"max_lane_iterations": n_max, "lane_iteration_latency_ms": 1e3 * lat, "run_seconds_per_step": run_s,
+           "share_of_solve": run_s / (leg.elapsed / steps)}
+    sclk = (leg.box or {}).get("sclk_mhz")
+    if sclk:
+        rec["cycles_per_stage_at_sclk"] = {"mean": lat * sclk[0] * 1e6 / T, "max": lat * sclk[2] * 1e6 / T}
+    return rec
+
+
 def outcome_record(res) -> dict:
     """Per-lane outcomes of a solve: statuses, iteration range, rollouts and the per-lane extra Armijo trials
     (rollouts beyond one per iteration) binned."""
@@ -705,6 +725,7 @@ def main():
             "warmup": 1, "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
             "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
             "roofline": None if r2 is None else {k: r2[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
+            "chain": persistent_chain_record(leg, k2, T),
             "note": "BASELINE cfg 2: 4,096 lanes on one GPU (64 wavefronts of lanes on 1,024 SIMDs: latency-bound, "
                     "the persistent schedule); --batch 4096 makes it the main line"}
         leg.free()

@@ -84,3 +84,21 @@ def test_stress_tail_record_critical_path():
     # no tail: the record keeps its keys without a bound
     leg.tail_iters_max = 0
     assert bench.stress_tail_record(leg, {}, 500)["seconds_per_step"] is None
+
+
+def test_persistent_chain_record():
+    """The cfg 2 leg's bound: the persistent kernel's seconds per solve over the longest lane's iterations is one
+    lane-iteration's chain latency; at the leg's SCLK that is the chain's cycles per stage."""
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    res = types.SimpleNamespace(n_iter=torch.tensor([390, 404, 12]))
+    leg = types.SimpleNamespace(steps=5, res=res, elapsed=5 * 0.2017, box={"sclk_mhz": [2390.0, 2380.0, 2400.0]})
+    ks = {"run": {"avg_ms": 49.7, "launches": 20}}
+    r = bench.persistent_chain_record(leg, ks, 500)
+    run_s = 49.7 * 20 / 1e3 / 5
+    assert np.isclose(r["run_seconds_per_step"], run_s) and r["max_lane_iterations"] == 404
+    assert np.isclose(r["lane_iteration_latency_ms"], 1e3 * run_s / 404)
+    assert np.isclose(r["share_of_solve"], run_s / 0.2017)
+    assert np.isclose(r["cycles_per_stage_at_sclk"]["mean"], run_s / 404 * 2390e6 / 500)
+    assert bench.persistent_chain_record(leg, {}, 500) == {}
