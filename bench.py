@@ -201,15 +201,23 @@ class NewtonLeg:
         self.x0_all = make_x0(self.total, spread=a.spread if spread is None else spread)
         lo, hi = gd.shard_range(self.total, self.rank, self.world)
         sched = {"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule]
+        import torch
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         self.solver = BatchedNewtonSolver(
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
             schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
             split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes, world_size=self.world,
             compact=None if a.compact == "auto" else a.compact == "on", **solver_kw)
+        torch.cuda.synchronize()
+        # construction: buffers (and, with placement selection, the further stream sets the first solve probes; a set
+        # pooled by an earlier solver of this shape is taken instead)
+        self.setup_s = time.perf_counter() - t0
         if timing:
             self.solver.enable_timing()
         self.x0_dev = eng.t(self.x0_all[lo:hi])          # inputs resident in HBM before the timed region
+        self.first_solve = None
         base = gd.make_reduce_stats()
         self.reduce = gd.TimedReduce(base) if base is not None else None
         self.a, self.gd = a, gd
@@ -217,8 +225,11 @@ class NewtonLeg:
     def run(self, steps: int, warmup: int, box=None):
         import torch
         a, gd, solver = self.a, self.gd, self.solver
-        for _ in range(warmup):
-            solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
+        for w in range(warmup):
+            r = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
+            if w == 0:    # the first solve of this solver (placement selection, if any, runs inside it)
+                self.first_solve = (r.seconds, r.lane_iterations)
+            r = None
         solver.reset_timing()
         if self.reduce is not None:
             self.reduce.reset()
@@ -234,6 +245,8 @@ class NewtonLeg:
             res = None                                   # free the previous solve's outputs first
             res = solver.solve(self.x0_dev, a.max_iters, reduce_stats=self.reduce, sync_every=a.sync_every)
             lane_its += res.lane_iterations
+            if self.first_solve is None:
+                self.first_solve = (res.seconds, res.lane_iterations)
             rolls += int(res.n_rollouts.sum().item())   # after the solve's own final synchronisation
             tail_its += res.tail_lane_iterations
             tail_iters_max = max(tail_iters_max, res.tail_iterations)
@@ -312,6 +325,19 @@ class NewtonLeg:
 
     def schedule(self) -> str:
         return self.res.schedule if self.res is not None else self.solver.schedule
+
+    def setup_record(self) -> dict:
+        """What a one-shot caller pays (the batched newton_Algorithm builds a solver per call): construction, and the
+        first solve (placement selection included); one_shot_value = its lane-iterations over both, all ranks."""
+        fs, fi = self.first_solve or (float("nan"), 0)
+        setup = self.gd.max_over_ranks(self.setup_s)
+        first = self.gd.max_over_ranks(fs)
+        its = self.gd.sum_over_ranks(fi)
+        rec = {"setup_s": setup, "first_solve_s": first, "one_shot_value": its / (setup + first),
+               "steady_solve_s": self.elapsed / max(self.steps, 1)}
+        if self.solver is not None and self.solver.placement:
+            rec["placement"] = dict(self.solver.placement)
+        return rec
 
     def free(self):
         import torch
@@ -658,11 +684,12 @@ def main():
         out["roofline"].update({k: v for k, v in roof.items() if k not in out["roofline"]})
         out["kernels"] = kern
     out["schedule"] = main_leg.schedule()
-    if main_leg.solver.placement:
-        # the stream-buffer placement the solver picked (BatchedNewtonSolver.select_placement)
-        out["placement"] = dict(main_leg.solver.placement, note=(
-            "stream-buffer sets probed at construction (24 iterations of the real schedule each, two rounds, ms per "
-            "iteration) and the one kept; outside the timed region"))
+    out["setup"] = dict(main_leg.setup_record(), note=(
+        "setup_s: solver construction (buffers, and the extra stream sets of placement selection); first_solve_s: the "
+        "first solve of the solver (warm-up; placement selection runs inside it: blocks of 12 iterations of that solve "
+        "on each stream set, the live state copied between sets, the fastest kept); one_shot_value: its "
+        "lane-iterations / (setup_s + first_solve_s), what one call of the batched newton_Algorithm achieves; "
+        "steady_solve_s: a timed solve.  placement.reused: the set came from the process's PlacementPool (DESIGN 6)"))
     if world > 1:
         # per-rank diagnostics of the main leg: a sub-linear scaling curve then says whether stragglers (spread of
         # the ranks' own elapsed times and lane-iterations), the statistics all-reduce or its read-back is the cause
@@ -696,7 +723,7 @@ def main():
             "lanes_per_gpu": -(-CFG4_LANES // world), "n_gpus": world, "steps": a.extra_steps, "warmup": 1,
             "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
             "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
-            "roofline_frac": None if r4 is None else r4["frac"],
+            "roofline_frac": None if r4 is None else r4["frac"], "setup": leg.setup_record(),
             "note": "BASELINE cfg 4: 1,048,576 lanes sharded over the ranks (one all-reduce of 8 fp64 stats per "
                     "host sync); max-over-ranks wall time"}
         leg.free()
@@ -746,7 +773,7 @@ def main():
             "low_occupancy": {"from_iteration": sv.serial_switch_at, "compactions_per_step":
                               leg.compactions / a.extra_steps,
                               "share_of_lane_iterations": leg.lowocc_lane_its / max(leg.lane_its, 1)},
-            "outcomes": outcome_record(leg.res),
+            "outcomes": outcome_record(leg.res), "setup": leg.setup_record(),
             "note": "SURVEY 8(d) stress variant: x0 = [th1, th2, 0, 0], th ~ U(+-1.5) (default_rng(0)), task-2 "
                     "settings, solved to convergence; the roofline is the phase kernel's over the lane-iterations "
                     "the phases ran (the tail and the low-occupancy regime are reported apart); decisions pinned "

@@ -29,6 +29,8 @@ from __future__ import annotations
 
 import ctypes as C
 import time
+import weakref
+from collections import OrderedDict
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -69,6 +71,48 @@ class SolveResult:
     tail_iterations: int = 0                # outer iterations the tail ran (its slowest lane's, up to the last one)
 
 
+class PlacementPool:
+    """Process-wide cache of the stream-buffer sets that placement selection chose (BatchedNewtonSolver._placement_*),
+    keyed by (device index, stream shapes).  A solver that chose a set leases it; when the solver is garbage-collected
+    the set comes back here, and the next solver of the same shape takes it without a probe or an allocation (the
+    batched newton_Algorithm builds a solver per call, bench.py one per leg).  At most one free set per key; free sets
+    beyond MAX_SHARE of the device's memory are dropped, oldest first.  ``clear()`` returns every free set to the
+    device."""
+    MAX_SHARE = 0.35
+    _free: "OrderedDict" = OrderedDict()
+
+    @staticmethod
+    def _bytes(key) -> int:
+        return 8 * sum(int(np.prod(sh)) for sh in key[1])
+
+    @classmethod
+    def take(cls, key):
+        """(streams, record) of a free set for ``key``, now leased to the caller, or None."""
+        return cls._free.pop(key, None)
+
+    @classmethod
+    def put(cls, key, streams, record):
+        if key in cls._free:
+            return
+        cls._free[key] = (streams, record)
+        try:
+            cap = cls.MAX_SHARE * torch.cuda.get_device_properties(key[0]).total_memory
+        except Exception:
+            return
+        while len(cls._free) > 1 and sum(cls._bytes(k) for k in cls._free) > cap:
+            cls._free.popitem(last=False)
+
+    @classmethod
+    def clear(cls):
+        cls._free.clear()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+
+    @classmethod
+    def held_bytes(cls) -> int:
+        return sum(cls._bytes(k) for k in cls._free)
+
+
 class BatchedNewtonSolver:
     """Owns the device buffers of a batch of ``B`` lanes that share x_ref / u_ref."""
 
@@ -86,14 +130,15 @@ class BatchedNewtonSolver:
     # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
     # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.
     TAIL_LANES_PER_CU = 4
-    # Placement selection (select_placement): the phase kernel's speed depends on where its six stream buffers land
-    # (one box: 1.92-2.06 ms per launch for six allocations alive at once, each stable for its lifetime;
-    # profiles/r05/placement/), so a large pipelined solver allocates up to this many stream sets, times a short
-    # probe of the real phase kernel on each and keeps the fastest (the same bits whichever it keeps).  Of the 12 sets
-    # probed in the round-5 final lines half were slow (4.10-4.40 ms per probe iteration against 3.95-4.01): four sets
-    # leave one selection in 16 on a slow placement, three one in 8 (profiles/r05/final*/bench.log "placement").
+    # Placement selection (see PlacementPool and _placement_tick): the phase kernel's speed depends on where its six
+    # stream buffers land (one box: 1.92-2.06 ms per launch for six allocations alive at once, each stable for its
+    # lifetime; profiles/r05/placement/), so a large pipelined solver holds up to this many stream sets during its
+    # first solve, runs blocks of PLACEMENT_BLOCK iterations of that solve on each (the live state copied from set to
+    # set between blocks: the same bits on any set) and keeps the fastest.  Of the 12 sets probed in the round-5 final
+    # lines half were slow (4.10-4.40 ms per probe iteration against 3.95-4.01): four sets leave one selection in 16
+    # on a slow placement, three one in 8 (profiles/r05/final*/bench.log "placement").
     PLACEMENT_TRIALS = 4
-    PLACEMENT_PROBE_ITERS = 24
+    PLACEMENT_BLOCK = 12
     # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
     # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
     CAND_SLOTS = 32768
@@ -149,7 +194,21 @@ class BatchedNewtonSolver:
         e = lambda *s, dt=F64: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
         Bp, N, T = self.Bp, self.N, self.T
         shapes = [(N, 2, Bp, 2), (N, 2, Bp, 2), (T, 2, Bp, 1), (T, 2, Bp, 1), (T, 2, Bp, 2), (T, 2, Bp, 1)]
-        if arena is not False and arena is not None:
+        self.pipeline = (sched_B >= self.pipeline_min_lanes(dev)) if pipeline is None else bool(pipeline)
+        # placement selection: default for the automatic schedule's pipelined solvers (the only schedule whose
+        # throughput is the HBM streams'); a set chosen by an earlier solver of this shape in this process is reused
+        # from the PlacementPool without a probe
+        if placement_trials is None:
+            placement_trials = (self.PLACEMENT_TRIALS if (auto_schedule and self.pipeline and persistent is not True
+                                                          and not arena and not checkpoint) else 1)
+        self.placement = None
+        self._pl = None
+        self._pool_key = (torch.device(dev).index, tuple(shapes))
+        pooled = PlacementPool.take(self._pool_key) if int(placement_trials) > 1 and not arena else None
+        if pooled is not None:
+            st, rec = pooled
+            self.placement = dict(rec, reused=True)
+        elif arena:
             # the six streams carved from one allocation, each 2 MiB aligned, in this order (arena: True = a torch
             # allocation, or a callable n -> fp64 device tensor of n elements that provides it)
             al = (2 << 20) // 8
@@ -171,7 +230,6 @@ class BatchedNewtonSolver:
         self.cand_ok = torch.zeros((max(int(max_ls), 1), Bp), dtype=torch.uint8, device=dev)
         self.partials = e(256 * 8)
         self.stats = torch.zeros(24, dtype=F64, device=dev)     # [0,8) totals, [8,16) / [16,24) halves
-        self.pipeline = (sched_B >= self.pipeline_min_lanes(dev)) if pipeline is None else bool(pipeline)
         self.max_iters = None
         self.hist_len = int(hist_len)
         self.hist_cost = torch.full((hist_len, Bp), float("nan"), dtype=F64, device=dev) if hist_len else None
@@ -294,79 +352,131 @@ class BatchedNewtonSolver:
         self._cap_pos = None
         self._cap_log = []
         self._sig_log = []
-        self.placement = None
-        if placement_trials is None:
-            placement_trials = (self.PLACEMENT_TRIALS if (auto_schedule and self.pipeline and not self.persistent and
-                                                          arena is False) else 1)
-        if int(placement_trials) > 1:
-            self.select_placement(int(placement_trials))
+        if self.placement is not None:            # a pooled set: back to the pool when this solver goes
+            self._lease_placement()
+        elif int(placement_trials) > 1 and self.pipeline and not self.persistent:
+            self._arm_placement(int(placement_trials))
 
-    def _set_streams(self, st):
-        """Use the stream set st = [x0, x1, u0, u1, K1, cs] (K1 and cs zeroed, as at construction)."""
+    def _set_streams(self, st, zero: bool = True):
+        """Use the stream set st = [x0, x1, u0, u1, K1, cs]; ``zero``: K1 and cs zeroed, as at construction (False: a
+        set that holds the live state, copied by _move_streams)."""
         self.x = list(st[0:2])
         self.u = list(st[2:4])                         # control planes (tau1, tau2)
         self.K1 = st[4]                                # gain row 1, pairs
         self.cs = st[5]                                # planes: cg = (u1 - K1 x) + gamma0 sigma1, sigma1
-        self.K1.zero_(); self.cs.zero_()
+        if zero:
+            self.K1.zero_(); self.cs.zero_()
         b = getattr(self, "batch", None)
         if b is not None:
             b.x[0], b.x[1] = self.x[0].data_ptr(), self.x[1].data_ptr()
             b.u[0], b.u[1] = self.u[0].data_ptr(), self.u[1].data_ptr()
             b.K1, b.cs = self.K1.data_ptr(), self.cs.data_ptr()
 
-    def select_placement(self, trials: int, iters: int | None = None) -> dict:
-        """Keep the fastest of up to ``trials`` stream-buffer placements.  The pipelined phase kernel moves its bytes at
-        a speed that depends on where its six streams land in HBM (one box, six allocations alive at once: 1.92 to
-        2.06 ms per launch, each stable over its lifetime; profiles/r05/placement/).  This allocates further stream
-        sets while the free memory allows (beside the lane-major results a solve allocates), runs ``iters``
-        iterations of the real schedule on a synthetic headline-like batch on each, timed with HIP events on the
-        solver's stream, keeps the fastest and releases the others.  Setup only: solve() re-initialises every buffer,
-        and every placement computes the same bits.  Records {"probe_ms": [...], "chosen": i} in ``self.placement``."""
-        iters = int(iters or self.PLACEMENT_PROBE_ITERS)
+    def _streams(self) -> list:
+        return [*self.x, *self.u, self.K1, self.cs]
+
+    def _move_streams(self, st):
+        """Continue on stream set ``st``: the six streams copied into it (stream-ordered device copies, ~19 GB each way
+        at 262,144 lanes), then the launches pointed at it.  Between two iterations the streams hold the whole state a
+        later iteration reads (both state / control buffers, the gains and offsets of the half whose sweep already ran),
+        so the solve continues bit for bit."""
+        for src, dst in zip(self._streams(), st):
+            dst.copy_(src)
+        self._set_streams(st, zero=False)
+
+    # --- placement selection ---------------------------------------------------------------
+    # Which placements are slow (profiles/r06/placement/): the slowness follows the RELATIVE placement of the streams the
+    # same waves touch in lock step -- on a slow set, replacing either K1 or cs by a fast set's copy makes it fast, while
+    # x0 / x1 / u0 / u1 do not matter, each buffer alone streams at the same rate wherever it lies, and the slow set shows
+    # ~2x the L2's fabric-side write / read-credit stalls and ~25% longer read latency at the same request counts, not
+    # more address-translation misses or any channel imbalance.  Which relative placements are bad is set by where the
+    # driver puts the pages, so the solver measures: up to PLACEMENT_TRIALS sets during the first solve, the fastest kept
+    # (and pooled for the process's later solvers of the same shape).
+    def _arm_placement(self, trials: int):
+        """Allocate up to ``trials`` - 1 further stream sets (while the free memory allows, beside the lane-major results
+        a solve allocates) for the online selection of the next solve (_placement_tick)."""
         dev = self.eng.device
-        e = lambda sh: torch.empty(sh, dtype=F64, device=dev)  # noqa: E731
         set_bytes = 8 * sum(int(np.prod(sh)) for sh in self._stream_shapes)
         B, N, T = self.B, self.N, self.T
         results_bytes = 8 * B * (4 * N + 2 * T + 8 * T + 2 * T)      # finalize's x, u, K, sigma
         free, _ = torch.cuda.mem_get_info(dev)
         k = min(int(trials), 1 + max(0, int((free - results_bytes - (4 << 30)) // max(set_bytes, 1))))
         if k < 2:
-            return {}
-        sets = [[*self.x, *self.u, self.K1, self.cs]] + [[e(sh) for sh in self._stream_shapes] for _ in range(k - 1)]
-        # a deterministic headline-like batch: th1, th2 spread over (-0.5, 0.5), at rest
-        lane = torch.arange(self.B, device=dev, dtype=F64)
-        x0 = torch.zeros((self.B, 4), dtype=F64, device=dev)
-        x0[:, 0] = torch.frac(lane * 0.6180339887498949) - 0.5
-        x0[:, 1] = torch.frac(lane * 0.7548776662466927) - 0.5
-        saved_launches = dict(self.launches)
-        # two round-robin rounds, each set's faster one kept: the first probe of a process also pays the clock ramp
-        # and first-launch costs (measured: the first of three probes ~4% slower whichever set it times)
-        times = [float("inf")] * k
-        for _ in range(2):
-            for i, st in enumerate(sets):
-                self._set_streams(st)
-                self.max_iters = iters + 1
-                self.init(x0)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                ev[0].record()
-                for _ in range(iters):
-                    self.iteration()
-                ev[1].record()
-                torch.cuda.synchronize(dev)
-                times[i] = min(times[i], ev[0].elapsed_time(ev[1]) / iters)
-        best = int(np.argmin(times))
-        self._set_streams(sets[best])
-        sets = None
-        self.max_iters = None
-        self.k = 0
-        self.launches = saved_launches
-        if self.timing is not None:
-            self.reset_timing()
-        for t in (self.hist_cost, self.hist_smax):
-            if t is not None:
-                t.fill_(float("nan"))
-        self.placement = {"trials": k, "probe_ms_per_iteration": times, "chosen": best}
-        return self.placement
+            return
+        t0 = time.perf_counter()
+        sets = [self._streams()] + [[torch.empty(sh, dtype=F64, device=dev) for sh in self._stream_shapes]
+                                    for _ in range(k - 1)]
+        self._pl = {"sets": sets, "cur": 0, "attempts": 0, "alloc_s": time.perf_counter() - t0}
+        self.placement = {"trials": k, "state": "pending", "alloc_s": self._pl["alloc_s"]}
+
+    def _placement_start(self):
+        """(init) A new solve: the selection schedule restarts from the set in use, in the order c, the others, then
+        the reverse (each set runs two blocks placed symmetrically, so a drift of the iterations' cost over the probe
+        cancels out of the comparison)."""
+        pl = self._pl
+        pl["attempts"] += 1
+        if pl["attempts"] > 2:                     # two solves ended before the probe did: keep the set in use
+            self._placement_finish(abandon=True)
+            return
+        k = len(pl["sets"])
+        seq = [pl["cur"]] + [i for i in range(k) if i != pl["cur"]]
+        pl.update(order=seq + seq[::-1], blocks=[], open=None, copies=0)
+
+    def _placement_tick(self):
+        """(iteration, before its launches) At the block boundaries of the schedule: close the running block with an
+        event, move the state to the next block's set, open the next block.  Only on the pipelined schedule while it
+        runs its phases (the low-occupancy regime and the tail end the probe for this solve)."""
+        pl = self._pl
+        if self._serial_now or self._run_now or "order" not in pl:
+            return
+        k, n = self.k, self.PLACEMENT_BLOCK
+        if k % n:
+            return
+        if pl["open"] is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            pl["blocks"].append((*pl["open"], ev))
+            pl["open"] = None
+        i = k // n
+        if i >= len(pl["order"]):
+            self._placement_finish()
+            return
+        target = pl["order"][i]
+        if target != pl["cur"]:
+            self._move_streams(pl["sets"][target])
+            pl["cur"] = target
+            pl["copies"] += 1
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        pl["open"] = (target, ev)
+
+    def _placement_finish(self, abandon: bool = False):
+        """Keep the fastest set (by the mean of its blocks' ms per iteration), release the others, and lease the kept
+        one to this solver (back to the PlacementPool when the solver goes)."""
+        pl, n = self._pl, self.PLACEMENT_BLOCK
+        per = {}
+        for s, e0, e1 in pl.get("blocks", []):
+            e1.synchronize()
+            per.setdefault(s, []).append(e0.elapsed_time(e1) / n)
+        best = pl["cur"]
+        if not abandon and per:
+            best = min(per, key=lambda s: sum(per[s]) / len(per[s]))
+            if best != pl["cur"]:
+                self._move_streams(pl["sets"][best])
+                pl["copies"] += 1
+        self.placement = {"trials": len(pl["sets"]), "state": "abandoned" if abandon else "chosen", "chosen": best,
+                          "ms_per_iteration": {int(s): v for s, v in sorted(per.items())},
+                          "probe_iterations": n * len(pl.get("blocks", [])), "copies": pl.get("copies", 0),
+                          "alloc_s": pl["alloc_s"], "at_iteration": int(self.k)}
+        self._pl = None
+        pl.clear()
+        torch.cuda.empty_cache()                    # the unused sets go back to the device, not the process's cache
+        self._lease_placement()
+
+    def _lease_placement(self):
+        st, rec = self._streams(), {k: v for k, v in self.placement.items() if k != "reused"}
+        f = weakref.finalize(self, PlacementPool.put, self._pool_key, st, rec)
+        f.atexit = False
 
     def ensure_cand_scratch(self) -> bool:
         """Allocate the candidate scratch (cand_slots slots, ~24 KiB each at T = 500) if this solver uses one and has
@@ -431,6 +541,8 @@ class BatchedNewtonSolver:
             self.xr_buf[:self.B] = self._xr_in if _ref_perm is None else self._xr_in[_ref_perm]
             self.ur_buf[:self.B] = self._ur_in if _ref_perm is None else self._ur_in[_ref_perm]
         self._x0 = x0
+        if self._pl is not None:
+            self._placement_start()
         _lib.check(self.eng.lib.gym_newton_init(C.byref(self.eng.model), C.byref(self.eng._w), x0.data_ptr(),
                                                 C.byref(self.batch), self.eng.stream), "gym_newton_init")
         self.k = 0
@@ -481,6 +593,8 @@ class BatchedNewtonSolver:
 
     def iteration(self) -> torch.Tensor:
         """Enqueue outer iteration k for every active lane; returns the 8 total statistics (device)."""
+        if self._pl is not None:
+            self._placement_tick()
         k = self.k
         if self.persistent or self._run_now:
             self._run(k, k + 1)
@@ -888,15 +1002,24 @@ def newton_loop(stepper, max_iters: int, reduce_stats=None, sync_every: int = 1,
 def _tail_rank_ok(stepper, host, local, reduce_stats) -> bool:
     """The per-rank part of the straggler-tail switch: the largest rank's active count within ``tail_lanes_rank``
     (None: no per-rank budget).  Sharded, the maximum is one MAX all-reduce (``reduce_stats.max_of``) that every rank
-    issues at the same iteration; a reduce without it compares the global count (>= every rank's) instead."""
+    issues at the same iteration; with a reducer that has no ``max_of`` the budget is not applied (a warning)."""
     cap = getattr(stepper, "tail_lanes_rank", None)
     if cap is None:
         return True
     if reduce_stats is None:
         return host[0] <= cap
     max_of = getattr(reduce_stats, "max_of", None)
+    if max_of is None:
+        # a caller-supplied reducer without a MAX: the per-rank budget cannot be checked without a collective the
+        # other ranks would not pair, so the global threshold alone decides (comparing the global count with the
+        # per-rank cap would delay the tail until the whole job fits one rank's budget)
+        if not getattr(stepper, "_warned_no_max_of", False):
+            import warnings
+            warnings.warn("reduce_stats has no max_of: the straggler tail's per-rank budget is not applied")
+            stepper._warned_no_max_of = True
+        return True
     n = float(local[0].item()) if isinstance(local, torch.Tensor) else float(np.asarray(local)[0])
-    return (max_of(n) if max_of is not None else host[0]) <= cap
+    return max_of(n) <= cap
 
 
 def tail_loop(solver, k: int, max_iters: int, reduce_stats, log_every: int, keep_stats: bool) -> list:

@@ -707,23 +707,51 @@ def test_per_lane_references(golden, task2_refs):
 
 
 def test_placement_selection_is_invisible(task2_refs):
-    """BatchedNewtonSolver.select_placement (round 5: up to three stream-buffer sets, a short probe of the real schedule
-    on each, the fastest kept) changes where the streams live, not what they compute: the solve after selection is
-    bit for bit the solve of a solver that kept its first allocation, on a batch with backtracking, LS-failure and
-    NaN lanes and per-lane histories (which the probe must not leave behind)."""
+    """Placement selection (round 6: the first solve runs blocks of PLACEMENT_BLOCK iterations on each of up to
+    PLACEMENT_TRIALS stream-buffer sets, the live state copied from set to set, and keeps the fastest) changes where the
+    streams live, not what they compute: the solve that selects is bit for bit the solve of a solver that kept its
+    first allocation, on a batch with backtracking, LS-failure and NaN lanes and per-lane histories.  The chosen set is
+    pooled for the process (PlacementPool): a second solver of the same shape takes it at construction (no probe, no
+    allocation of streams: < 50 ms) and solves to the same bits."""
+    import gc
+    import time
+    import torch
     from gymnast_optimalcontrol_amd.engine import AcrobotEngine
-    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver, PlacementPool
     xr, ur, _ = task2_refs
     B, H = 2000, 120
     x0 = np.zeros((B, 4)); x0[:, :2] = np.random.default_rng(5).uniform(-1.5, 1.5, (B, 2))
     x0[11] = np.nan
     eng = AcrobotEngine()
     kw = dict(tol=1e-4, gamma_0=1.0, pipeline=True, hist_len=H)     # gamma_0 = 1: wide starts backtrack early
+    trials = BatchedNewtonSolver.PLACEMENT_TRIALS
+    assert trials * 2 * BatchedNewtonSolver.PLACEMENT_BLOCK < H
+    PlacementPool.clear()
     a = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=1, **kw)
-    s = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=3, **kw)
-    assert a.placement is None and s.placement["trials"] >= 2 and 0 <= s.placement["chosen"] < s.placement["trials"]
-    assert s.x[0].data_ptr() == s.batch.x[0] and s.K1.data_ptr() == s.batch.K1 and s.cs.data_ptr() == s.batch.cs
+    s = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=trials, **kw)
+    assert a.placement is None and s.placement["state"] == "pending" and s.placement["trials"] == trials
     ra, rs = a.solve(x0, H), s.solve(x0, H)
-    for name in ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax"):
+    assert s.placement["state"] == "chosen" and 0 <= s.placement["chosen"] < trials, s.placement
+    assert s.placement["probe_iterations"] == 2 * trials * BatchedNewtonSolver.PLACEMENT_BLOCK
+    assert s.x[0].data_ptr() == s.batch.x[0] and s.K1.data_ptr() == s.batch.K1 and s.cs.data_ptr() == s.batch.cs
+    names = ("x", "u", "K", "sigma", "cost", "n_iter", "status", "n_rollouts", "gamma", "hist_cost", "hist_smax")
+    for name in names:
         assert np.array_equal(getattr(ra, name).cpu().numpy(), getattr(rs, name).cpu().numpy(), equal_nan=True), name
     assert (ra.n_rollouts > ra.n_iter).sum().item() > 10 and (ra.status == 2).sum().item() > 0
+    chosen_ptr = s.K1.data_ptr()
+    del s, rs
+    gc.collect()
+    assert PlacementPool.held_bytes() > 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s2 = BatchedNewtonSolver(eng, xr, ur, B, placement_trials=trials, **kw)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    assert s2.placement.get("reused") and s2.K1.data_ptr() == chosen_ptr and setup < 0.05, (s2.placement, setup)
+    r2 = s2.solve(x0, H)
+    for name in names:
+        assert np.array_equal(getattr(ra, name).cpu().numpy(), getattr(r2, name).cpu().numpy(), equal_nan=True), name
+    del s2
+    gc.collect()
+    PlacementPool.clear()
+    assert PlacementPool.held_bytes() == 0

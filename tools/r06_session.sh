@@ -1,0 +1,51 @@
+#!/bin/bash
+# Round-6 GPU session: named steps, each under its own time limit, chained so that the first failure (a test
+# failure, a fault, an abort, a time limit) ends the script.  Output under gpurun_out/r06/<tag>/<name>.log.
+#   R06_TAG=place tools/r06_session.sh avail place p_utcl p_lat p_tccstall p_tcc
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+OUT=gpurun_out/r06/${R06_TAG:-run}
+mkdir -p $OUT
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a $OUT/steps.log
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] end $name rc=$rc" | tee -a $OUT/steps.log
+  tail -4 "$OUT/$name.log" | cut -c1-400
+  return $rc
+}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+PP="python3 -u tools/placement_pmc.py --sets ${PSETS:-6}"
+pmc() {  # pmc <name> <format> <counters...>: one rocprofv3 pass over tools/placement_pmc.py, then its summary
+  local name=$1 fmt=$2; shift 2
+  step $name 300 rocprofv3 --pmc "$@" --kernel-include-regex k_nt_phase -d $OUT/$name -o run --output-format $fmt \
+    -- $PP --out $OUT/$name/run.json || return $?
+  step ${name}_parse 120 python3 -u tools/placement_pmc_parse.py $OUT/$name $OUT/$name/run.json $OUT/$name/summary.json \
+    || return $?
+  rm -f $OUT/$name/*/*.db $OUT/$name/*.db 2>/dev/null
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    avail) step list_avail 120 rocprofv3 --list-avail || exit $? ;;
+    place) step place 300 $PP --out $OUT/place.json || exit $? ;;
+    place2) step place2 300 $PP --out $OUT/place2.json || exit $? ;;
+    scan) step scan 400 python3 -u tools/placement_scan.py --out $OUT/scan.json || exit $? ;;
+    p_utcl) pmc p_utcl csv TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum \
+              TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE || exit $? ;;
+    p_lat) pmc p_lat csv TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum \
+              TCP_TCR_TCP_STALL_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum || exit $? ;;
+    p_tccstall) pmc p_tccstall csv TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum TCC_TAG_STALL_sum \
+              TCC_BUSY_sum || exit $? ;;
+    p_tcc) pmc p_tcc "csv rocpd" TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ_LEVEL || exit $? ;;
+    ptest) step pytest_place 300 $PYT tests/test_gpu_parity.py -m gpu -k placement || exit $? ;;
+    benchmain) step benchmain 400 python -u bench.py --steps 3 --warmup 1 --no-cpu --extra-legs "" || exit $? ;;
+    tests) step pytest_gpu 1100 $PYT tests -m gpu || exit $? ;;
+    smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) step bench 600 python -u bench.py || exit $? ;;
+    bench20) step bench20 600 python -u bench.py --steps 20 --warmup 2 --extra-legs "" || exit $? ;;
+    trace3) step trace_cfg3 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg3 -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
