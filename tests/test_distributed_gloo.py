@@ -1,4 +1,4 @@
-"""Multi-rank lane sharding on CPU (torch.distributed gloo, world_size 2, 3 and 7).
+"""Multi-rank lane sharding on CPU (torch.distributed gloo, world_size 2, 3, 7 and 8 -- the driver's node).
 
 The product's outer loop (solver.newton_loop) and sharding/all-reduce helpers (distributed.py)
 drive a per-shard engine; here the engine is the oracle's NewtonStepper so the multi-rank logic is
@@ -17,14 +17,14 @@ N_SHORT = 61          # a 1.2 s horizon keeps the NumPy oracle fast; the algorit
 MAX_ITERS = 40
 
 
-def _problem():
+def _problem(lanes=7):
     from conftest import GOLDEN
     from oracle.acrobot_np import load_task2_refs
     x_ref, u_ref, _ = load_task2_refs(os.path.join(GOLDEN, "task2_input_fully_actuated.npz"))
     x_ref, u_ref = x_ref[:N_SHORT], u_ref[:N_SHORT - 1]
     rng = np.random.default_rng(7)
-    x0 = np.zeros((7, 4))
-    x0[:, :2] = rng.uniform(-1.5, 1.5, (7, 2))
+    x0 = np.zeros((lanes, 4))
+    x0[:, :2] = rng.uniform(-1.5, 1.5, (lanes, 2))
     x0[3] = np.nan                       # a lane that fails on its first iteration
     return x0, x_ref, u_ref
 
@@ -35,7 +35,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, lanes):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -46,7 +46,7 @@ def _worker(rank, world, port, out_path):
     from gymnast_optimalcontrol_amd.solver import newton_loop
     from oracle.acrobot_np import NewtonStepper
     gd.init_process_group(backend="gloo")
-    x0, x_ref, u_ref = _problem()
+    x0, x_ref, u_ref = _problem(lanes)
     lo, hi = gd.shard_range(len(x0), rank, world)
     st = NewtonStepper(x0[lo:hi], x_ref, u_ref, tol=1e-4, gamma_0=0.1)
     log = newton_loop(st, MAX_ITERS, reduce_stats=gd.make_reduce_stats(), keep_stats=True)
@@ -59,15 +59,17 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 7])   # 7: one lane per rank, the NaN lane alone on its rank
-def test_sharded_loop_matches_single_process(tmp_path, world):
+# 7: one lane per rank, the NaN lane alone on its rank; 8: the driver's node, 11 ragged lanes (2,2,2,1,1,1,1,1)
+@pytest.mark.parametrize("world,lanes", [(2, 7), (3, 7), (7, 7), (8, 11)])
+def test_sharded_loop_matches_single_process(tmp_path, world, lanes):
     from gymnast_optimalcontrol_amd.solver import newton_loop
     from oracle.acrobot_np import NewtonStepper
     out = str(tmp_path / "gathered.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), out, lanes), nprocs=world, join=True,
+                       start_method="spawn")
     parts = np.load(out, allow_pickle=True)          # written by this test's own workers
 
-    x0, x_ref, u_ref = _problem()
+    x0, x_ref, u_ref = _problem(lanes)
     ref = NewtonStepper(x0, x_ref, u_ref, tol=1e-4, gamma_0=0.1)
     ref_log = np.asarray(newton_loop(ref, MAX_ITERS, keep_stats=True))
     r = ref.result()
@@ -122,7 +124,7 @@ class _PersistentAdapter:
         pass
 
 
-def _persistent_worker(rank, world, port, out_path, chunk):
+def _persistent_worker(rank, world, port, out_path, chunk, lanes):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -133,7 +135,7 @@ def _persistent_worker(rank, world, port, out_path, chunk):
     from gymnast_optimalcontrol_amd.solver import run_loop
     from oracle.acrobot_np import NewtonStepper
     gd.init_process_group(backend="gloo")
-    x0, x_ref, u_ref = _problem()
+    x0, x_ref, u_ref = _problem(lanes)
     lo, hi = gd.shard_range(len(x0), rank, world)
     ad = _PersistentAdapter(NewtonStepper(x0[lo:hi], x_ref, u_ref, tol=1e-4, gamma_0=0.1), chunk)
     log = run_loop(ad, MAX_ITERS, gd.make_reduce_stats(), 0, True)
@@ -151,17 +153,17 @@ def _persistent_worker(rank, world, port, out_path, chunk):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk", [(2, 4), (3, 7)])
-def test_persistent_loop_sharded_matches_single_process(tmp_path, world, chunk):
+@pytest.mark.parametrize("world,chunk,lanes", [(2, 4, 7), (3, 7, 7), (8, 5, 11)])
+def test_persistent_loop_sharded_matches_single_process(tmp_path, world, chunk, lanes):
     """The persistent schedule's host loop across ranks: one all-reduce per launch of ``chunk`` iterations on
     every rank (ragged shards), the global stop after the launch in which the last lane of any rank finished,
     and per-lane results equal to the single-process solve."""
     from oracle.acrobot_np import NewtonStepper
     out = str(tmp_path / "gathered.npy")
-    mp.start_processes(_persistent_worker, args=(world, _free_port(), out, chunk), nprocs=world, join=True,
+    mp.start_processes(_persistent_worker, args=(world, _free_port(), out, chunk, lanes), nprocs=world, join=True,
                        start_method="spawn")
     parts = np.load(out, allow_pickle=True)          # written by this test's own workers
-    x0, x_ref, u_ref = _problem()
+    x0, x_ref, u_ref = _problem(lanes)
     ref = NewtonStepper(x0, x_ref, u_ref, tol=1e-4, gamma_0=0.1)
     from gymnast_optimalcontrol_amd.solver import newton_loop
     newton_loop(ref, MAX_ITERS)
@@ -254,7 +256,8 @@ def _tail_worker(rank, world, port, out_path):
     from gymnast_optimalcontrol_amd.solver import newton_loop
     from host_loop_mock import MockSolver
     gd.init_process_group(backend="gloo")
-    need = {0: [5, 60, 61], 1: [100, 7, 8, 9]}[rank]     # rank 0 alone would switch earlier than rank 1
+    # rank 0 alone would switch earlier than rank 1; ranks 2.. (8-rank runs) finish early
+    need = {0: [5, 60, 61], 1: [100, 7, 8, 9]}.get(rank, [3, 4, 5 + rank])
     s = MockSolver(need, tail_lanes=2, tail_chunk=16)
     calls = []
     red = gd.make_reduce_stats()
@@ -273,19 +276,22 @@ def _tail_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_tail_switch_is_global_across_ranks(tmp_path):
-    """Two ranks with different local stragglers switch to the tail at the same iteration (the all-reduced active
-    count decides), issue the same collectives at the same iterations, and each ends with its lanes' counts."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_tail_switch_is_global_across_ranks(tmp_path, world):
+    """Ranks with different local stragglers switch to the tail at the same iteration (the all-reduced active count
+    decides), issue the same collectives at the same iterations, and each ends with its lanes' counts; at 8 ranks six
+    of them have finished long before and still pair every collective."""
     import json
     out = str(tmp_path / "tail.json")
-    mp.start_processes(_tail_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_tail_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
     g = json.load(open(out))
-    t0 = [tuple(e) for e in g[0]["events"] if e[0] == "tail"]
-    t1 = [tuple(e) for e in g[1]["events"] if e[0] == "tail"]
-    # global active after k = 60: rank 0 {61} + rank 1 {100} = 2 -> both switch at 60 (rank 0 alone: at 8)
-    assert t0 == t1 and t0[0] == ("tail", 60, 76) and t0[-1][2] >= 100
-    assert g[0]["calls"] == g[1]["calls"]                 # paired collectives
+    tails = [[tuple(e) for e in g[r]["events"] if e[0] == "tail"] for r in range(world)]
+    # global active after k = 60: rank 0 {61} + rank 1 {100} = 2 -> every rank switches at 60 (rank 0 alone: at 8)
+    assert all(t == tails[0] for t in tails) and tails[0][0] == ("tail", 60, 76) and tails[0][-1][2] >= 100
+    assert all(g[r]["calls"] == g[0]["calls"] for r in range(world))       # paired collectives
     assert g[0]["n_iter"] == [5, 60, 61] and g[1]["n_iter"] == [100, 7, 8, 9]
+    for r in range(2, world):
+        assert g[r]["n_iter"] == [3, 4, 5 + r]
 
 
 def _tail_budget_worker(rank, world, port, out_path):
@@ -299,7 +305,8 @@ def _tail_budget_worker(rank, world, port, out_path):
     from gymnast_optimalcontrol_amd.solver import newton_loop
     from host_loop_mock import MockSolver
     gd.init_process_group(backend="gloo")
-    need = {0: [5, 60, 61, 62], 1: [7, 8, 9, 100]}[rank]   # skewed: rank 0 holds three stragglers
+    # skewed: rank 0 holds three stragglers; ranks 2.. (8-rank runs) one lane each that finishes early
+    need = {0: [5, 60, 61, 62], 1: [7, 8, 9, 100]}.get(rank, [3 + rank])
     s = MockSolver(need, tail_lanes=4, tail_chunk=16)
     s.tail_lanes_rank = 2                                  # the solver's default: a per-GPU budget
     red = gd.TimedReduce(gd.make_reduce_stats())           # forwards max_of, as bench.py's wrapper does
@@ -314,20 +321,24 @@ def _tail_budget_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_tail_switch_waits_for_every_rank_within_its_budget(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_tail_switch_waits_for_every_rank_within_its_budget(tmp_path, world):
     """with skewed shards the global count can be under the threshold while one rank still holds more
     than its per-GPU budget of active lanes; the switch then waits (one MAX all-reduce of the local counts, issued by
-    every rank at the same iteration) until the largest rank is within it."""
+    every rank at the same iteration) until the largest rank is within it.  At 8 ranks the MAX over the seven other
+    ranks' counts (0 or 1) must not hide rank 0's 3."""
     import json
     out = str(tmp_path / "tail_budget.json")
-    mp.start_processes(_tail_budget_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_tail_budget_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
     g = json.load(open(out))
-    t0 = [tuple(e) for e in g[0]["events"] if e[0] == "tail"]
-    t1 = [tuple(e) for e in g[1]["events"] if e[0] == "tail"]
-    # after k = 12: global 3 + 1 = 4 <= 4 but rank 0 holds 3 > 2; after k = 60: 2 + 1, max 2 -> both switch at 60
-    assert t0 == t1 and t0[0] == ("tail", 60, 76)
-    assert g[0]["calls"] == g[1]["calls"]
+    tails = [[tuple(e) for e in g[r]["events"] if e[0] == "tail"] for r in range(world)]
+    # after k = 12: global 3 + 1 = 4 <= 4 but rank 0 holds 3 > 2; after k = 60: 2 + 1, max 2 -> all switch at 60
+    assert all(t == tails[0] for t in tails) and tails[0][0] == ("tail", 60, 76)
+    assert all(g[r]["calls"] == g[0]["calls"] for r in range(world))
     assert g[0]["n_iter"] == [5, 60, 61, 62] and g[1]["n_iter"] == [7, 8, 9, 100]
+    for r in range(2, world):
+        assert g[r]["n_iter"] == [3 + r]
 
 
 def _timed_worker(rank, world, port, out_path):
