@@ -190,16 +190,72 @@ def mpc_line(a, B, steps, warmup, cpu_lanes):
     return out
 
 
+def cfg1_line(repeats: int = 2) -> dict:
+    """BASELINE cfg 1 through the drop-in: main.task_2's own call (/root/reference/main.py:52-71),
+    tg.newton_Algorithm(np.zeros(4), x_ref, u_ref, max_iters=5000, tol=1e-4, gamma_0=0.1, plot_armijo_iters=7) on
+    the reference-named module (one lane; the reference's history -- every iterate and sigma -- copied to the host
+    after each iteration, as the reference keeps it), timed end to end after one untimed warm-up call.  The Armijo
+    report figures of the first iterations are drawn when matplotlib is importable (Agg); their time is reported
+    apart, since the reference's 78.3 s was measured with the plotting function stubbed."""
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    from gymnast_optimalcontrol_amd import trajectory_generation as tg
+    x_ref, u_ref, _ = tg.get_fully_actuated_ref(os.path.join(ROOT, "gymnast_optimalcontrol_amd", "data",
+                                                              "fully_actuated_trajectory.npz"))
+    plot_s = [0.0]
+    orig = tg.plot_armijo_line_search
+
+    def timed_plot(*args, **kw):
+        t = time.perf_counter()
+        try:
+            return orig(*args, **kw)
+        finally:
+            plot_s[0] += time.perf_counter() - t
+    tg.plot_armijo_line_search = timed_plot
+    try:
+        tg.newton_Algorithm(np.zeros(4), x_ref, u_ref, max_iters=3, tol=1e-4, gamma_0=0.1, plot_armijo_iters=7,
+                            verbose=False)
+        runs = []
+        for _ in range(repeats):
+            plot_s[0] = 0.0
+            t0 = time.perf_counter()
+            x, u, K, sigma, hist = tg.newton_Algorithm(np.zeros(4), x_ref, u_ref, max_iters=5000, tol=1e-4,
+                                                       gamma_0=0.1, plot_armijo_iters=7, verbose=False)
+            runs.append((time.perf_counter() - t0, plot_s[0]))
+    finally:
+        tg.plot_armijo_line_search = orig
+        try:
+            import matplotlib.pyplot as plt
+            plt.close("all")
+        except ImportError:
+            pass
+    g = np.load(os.path.join(ROOT, "tests", "golden", "task2_reference_output.npz"))
+    its = len(hist["sigma_norm"])
+    sec, psec = min(runs, key=lambda r: r[0])
+    return {"seconds": sec, "plot_seconds": psec, "seconds_without_plots": sec - psec, "iterations": its,
+            "iterations_per_s": its / sec, "repeats": [r[0] for r in runs],
+            "parity": {"rel_l2_x": float(np.linalg.norm(x - g["x"]) / np.linalg.norm(g["x"])),
+                       "rel_l2_u": float(np.linalg.norm(u - g["u"]) / np.linalg.norm(g["u"])), "tolerance": 1e-8},
+            "reference_seconds": 78.3, "reference_iterations": 393,
+            "speedup_vs_reference_without_plots": 78.3 / (sec - psec),
+            "note": "main.task_2's call on the drop-in module (one lane, host history every iteration); reference: "
+                    "the same call on one core of the survey container with its plotting stubbed (SURVEY 3.1), not "
+                    "re-measured on this box"}
+
+
 class NewtonLeg:
     """One timed configuration of the batched solver on this rank: ``total`` global lanes of the bench workload,
     this rank's contiguous shard, the schedule chosen on the largest shard (identical on every rank)."""
 
-    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None, spread=None, **solver_kw):
+    def __init__(self, a, gd, eng, x_ref, u_ref, total: int, timing: bool, u0_zero=None, spread=None, shard=None,
+                 **solver_kw):
+        """``shard`` = (r, W): this process solves rank r's shard of a W-rank job alone (a one-GPU rehearsal of one
+        rank's workload: its lanes, and the schedule every rank of that job picks)."""
         from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
         self.rank, self.world = gd.rank_world()
         self.total = int(total)
         self.x0_all = make_x0(self.total, spread=a.spread if spread is None else spread)
-        lo, hi = gd.shard_range(self.total, self.rank, self.world)
+        srank, sworld = shard if shard is not None else (self.rank, self.world)
+        lo, hi = gd.shard_range(self.total, srank, sworld)
         sched = {"auto": None, "serial": False, "pipelined": True, "persistent": None}[a.schedule]
         import torch
         torch.cuda.synchronize()
@@ -207,7 +263,7 @@ class NewtonLeg:
         self.solver = BatchedNewtonSolver(
             eng, x_ref, u_ref, hi - lo, tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, pipeline=sched,
             persistent={"auto": None, "persistent": True}.get(a.schedule, False), chunk=a.chunk,
-            schedule_lanes=gd.schedule_lanes(self.total, self.world), u0_zero=u0_zero,
+            schedule_lanes=gd.schedule_lanes(self.total, sworld), u0_zero=u0_zero,
             split_waves=a.split_waves == "on", tail_lanes=a.tail_lanes, world_size=self.world,
             compact=None if a.compact == "auto" else a.compact == "on", **solver_kw)
         torch.cuda.synchronize()
@@ -528,12 +584,14 @@ def main():
                     help="newton: the north-star metric (cfg 3 per GPU, weak scaling); cfg4: 1,048,576 lanes "
                          "strong-scaled over the ranks; mpc: BASELINE cfg 5; stress: the cfg 3 batch with "
                          "th ~ U(+-1.5) (SURVEY 8(d)'s stress variant: backtracking and Armijo failures)")
-    ap.add_argument("--extra-legs", default="cfg4,general,cfg2,mpc,stress",
+    ap.add_argument("--extra-legs", default="cfg4,cfg4share,general,cfg2,mpc,stress,cfg1",
                     help="comma list of secondary timed legs reported inside the same JSON line (newton "
                          "workload): cfg4 = 1,048,576 lanes strong-scaled over the ranks; general = the same "
                          "workload on the general (tau1-streaming) kernels, N=1 only; cfg2 = BASELINE cfg 2 "
                          "(4,096 lanes, N=1 only); mpc = BASELINE cfg 5 (N=1 only); stress = SURVEY 8(d)'s "
-                         "stress variant (th ~ U(+-1.5), N=1 only); '' for none")
+                         "stress variant (th ~ U(+-1.5), N=1 only); cfg4share = one rank's share of cfg 4 at N = 8 "
+                         "(131,072 lanes, N=1 only); cfg1 = main.task_2's call through the drop-in module (N=1 "
+                         "only); '' for none")
     ap.add_argument("--extra-steps", type=int, default=2, help="timed solves of each extra leg (1 warmup)")
     ap.add_argument("--horizon", type=int, default=50, help="MPC prediction horizon T_pred (cfg 5: 50)")
     ap.add_argument("--schedule", choices=("auto", "serial", "pipelined", "persistent"), default="auto",
@@ -779,6 +837,23 @@ def main():
                     "the phases ran (the tail and the low-occupancy regime are reported apart); decisions pinned "
                     "lane by lane against the C oracle (tests/test_gpu_stress.py)"}
         leg.free()
+    if "cfg4share" in legs and world == 1:
+        # the per-GPU workload of cfg 4 at N = 8 (rank 0's 131,072 lanes of the 1,048,576-lane batch, the schedule
+        # every rank of that job picks: exactly the pipelined threshold, 512 lanes per CU) on this one GPU
+        leg = NewtonLeg(a, gd, eng, x_ref, u_ref, CFG4_LANES, not a.no_timing, shard=(0, 8)).run(a.extra_steps, 1, box)
+        box_legs["cfg4_rank_share"] = leg.box
+        ksh, rsh = leg.kernel_report(N)
+        out["cfg4_rank_share"] = {
+            "value": leg.value, "unit": "Newton iterations/s", "lanes": leg.solver.B, "steps": a.extra_steps,
+            "warmup": 1, "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
+            "roofline": None if rsh is None else {k: rsh[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
+            "setup": leg.setup_record(),
+            "note": "one rank's share of BASELINE cfg 4 at N = 8 (lanes [0, 131072) of the cfg 4 batch), solved alone "
+                    "on this GPU: the per-GPU workload and schedule of the 8-GPU run, without its all-reduces"}
+        leg.free()
+    if "cfg1" in legs and world == 1:
+        out["cfg1_drop_in"] = cfg1_line()
     if "mpc" in legs and world == 1:
         m = mpc_line(a, 8192, max(a.extra_steps, 3), 1, 0)
         out["mpc_cfg5"] = {k: m[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "kernels",

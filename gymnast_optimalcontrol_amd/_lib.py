@@ -32,7 +32,7 @@ EXPORTS = (
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run",
                 "tail")
 
-ABI_VERSION = 14        # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 15        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT

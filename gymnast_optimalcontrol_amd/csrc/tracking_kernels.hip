@@ -261,18 +261,22 @@ __device__ __forceinline__ double riccati_map_lane(double P, const MapLane& c, d
 constexpr int kMpcMaxStages = 256;   // LDS stage table of one workgroup: its 4 windows' stages (L + 2 <= 256)
 
 // ------------------------------------------------------------------------------------------
-// compute_P_inf (:144-165) by doubling (the structure-preserving doubling algorithm for the DARE,
-// P = Q + A'PA - A'PB (R + B'PB)^-1 B'PA):  A_0 = A, G_0 = B R^-1 B', H_0 = Q, and with W = (I + G_k H_k)^-1
-//   A_{k+1} = A_k W A_k,   G_{k+1} = G_k + A_k W G_k A_k',   H_{k+1} = H_k + A_k' H_k W A_k,
-// H_k is the reference's fixed-point iterate after 2^k maps from P = Q (the horizon doubles each step), so ~10
-// doublings reach what the reference's loop reaches in ~434 dependent maps (the cfg 5 pad: P[0][0] ~ 2.26e7; the
-// reference stops where max|dP| < 1e-6, within ~9e-13 relative of the limit; the doubling lands on the limit).
+// compute_P_inf (:144-165) with doubling jumps.  The reference iterates the Riccati map F from P_0 = Q and stops at
+// the first n with max|P_{n+1} - P_n| < tol, returning P_{n+1}.  The structure-preserving doubling algorithm
+//   A_0 = A, G_0 = B R^-1 B', H_0 = Q;  W = (I + G_k H_k)^-1,
+//   A_{k+1} = A_k W A_k,   G_{k+1} = G_k + A_k W G_k A_k',   H_{k+1} = H_k + A_k' H_k W A_k
+// gives H_k = F^(2^k)(0) = P_{2^k - 1}, the reference's own iterate (up to rounding), in k steps.  k_mpc_gains jumps
+// with it while the map still moves H_k by >= tol (the reference has not stopped there yet) and then runs the
+// reference's loop, with its own test, from the last such H_k: the same stop iterate as the reference, ~2^(k-1)
+// maps instead of ~2^k (the cfg 5 pad: 434 maps -> 9 doublings + 179 maps).  Doubling all the way to the limit
+// (round 5) overshoots the reference's stop by ~tol rho^2 / (1 - rho^2) absolute, which is invisible at the cfg 5
+// pad's scale (P ~ 2e7) but not for smaller Q / R.
 // On a 16-lane group as the Riccati map below: lane 4i+j owns entry (i, j) of every 4x4 matrix; each product is one
 // round through a per-group LDS scratch (one wavefront: its LDS accesses are in order, so no barrier), W by
 // Gauss-Jordan elimination with partial pivoting (every lane finds the same pivot row).  Every group of every
 // workgroup computes the same bits.
 // ------------------------------------------------------------------------------------------
-constexpr int kSdaMaxSteps = 40;
+constexpr int kSdaMaxSteps = 30;   // 2^30 - 1 maps: beyond any max_iter an int holds
 
 __device__ __forceinline__ void wave_lds_order() {   // LDS writes of this wavefront visible to its later reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -289,83 +293,73 @@ __device__ __forceinline__ double dot_xyt(const double* X, const double* Y, int 
 __device__ __forceinline__ double dot_xty(const double* X, const double* Y, int i, int j) {
     return ((X[i] * Y[j] + X[4 + i] * Y[4 + j]) + X[8 + i] * Y[8 + j]) + X[12 + i] * Y[12 + j];
 }
-__device__ __forceinline__ double grp16_max(double v) {   // max over the lane's 16-lane group
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 16));
-    return v;
+
+// The doubling's initial triple on the pad (lane 4i+j: entry (i, j) of A_0, G_0, H_0)
+__device__ __forceinline__ void sda16_init(double h, const StageLin& pad, const M44& Q, const M22& R, int i, int j,
+                                           double& a, double& g, double& hh) {
+    // A_f: rows 0, 1 = [1 0 h 0], [0 1 0 h]; rows 2, 3 the StageLin's.  G_0 = (R^-1)[1][1] b b', b = (0, 0, b2, b3)'
+    a = i == 0 ? (j == 0 ? 1.0 : (j == 2 ? h : 0.0)) : i == 1 ? (j == 1 ? 1.0 : (j == 3 ? h : 0.0))
+                                                   : (i == 2 ? pad.a2[j] : pad.a3[j]);
+    const double r11 = R.v[0] / (R.v[0] * R.v[3] - R.v[1] * R.v[2]);
+    const double bi = i == 2 ? pad.b2 : (i == 3 ? pad.b3 : 0.0), bj = j == 2 ? pad.b2 : (j == 3 ? pad.b3 : 0.0);
+    g = r11 * bi * bj;
+    hh = Q.v[4 * i + j];
 }
 
-// The pad's P_inf by doubling; sm = this group's 8 x 16 doubles of LDS.  Returns the number of doublings with this
-// lane's entry of P in *P, or 0 if they did not settle (a zero / non-finite pivot, a non-finite H, no settling within
-// kSdaMaxSteps): the caller then runs the reference's fixed point.  Every lane of the wavefront must call it.
-__device__ int dare_sda16(double h, const StageLin& pad, const M44& Q, const M22& R, int i, int j, double* sm,
-                          double* P) {
+// One doubling step of (a, g, hh) in place; sm = this group's 8 x 16 doubles of LDS.  Returns false (for every lane of
+// the wavefront) on a zero / non-finite pivot or a non-finite H.  Every lane of the wavefront must call it.
+__device__ bool sda16_step(int i, int j, double* sm, double& a, double& g, double& hh) {
     double* sA = sm;        double* sG = sm + 16;  double* sH = sm + 32;  double* sM = sm + 48;
     double* sV = sm + 64;   double* sW = sm + 80;  double* sT = sm + 96;  double* sU = sm + 112;
     const int l = 4 * i + j;
-    // A_f: rows 0, 1 = [1 0 h 0], [0 1 0 h]; rows 2, 3 the StageLin's.  G_0 = (R^-1)[1][1] b b', b = (0, 0, b2, b3)'
-    double a = i == 0 ? (j == 0 ? 1.0 : (j == 2 ? h : 0.0)) : i == 1 ? (j == 1 ? 1.0 : (j == 3 ? h : 0.0))
-                                                            : (i == 2 ? pad.a2[j] : pad.a3[j]);
-    const double r11 = R.v[0] / (R.v[0] * R.v[3] - R.v[1] * R.v[2]);
-    const double bi = i == 2 ? pad.b2 : (i == 3 ? pad.b3 : 0.0), bj = j == 2 ? pad.b2 : (j == 3 ? pad.b3 : 0.0);
-    double g = r11 * bi * bj, hh = Q.v[l];
-    for (int step = 1; step <= kSdaMaxSteps; ++step) {
-        sA[l] = a; sG[l] = g; sH[l] = hh;
-        wave_lds_order();
-        double m = dot_xy(sG, sH, i, j) + (i == j ? 1.0 : 0.0);        // I + G H
-        double v = i == j ? 1.0 : 0.0;                                  // its inverse, built alongside
-        bool ok = true;
+    wave_lds_order();                                               // reads of the previous step before these writes
+    sA[l] = a; sG[l] = g; sH[l] = hh;
+    wave_lds_order();
+    double m = dot_xy(sG, sH, i, j) + (i == j ? 1.0 : 0.0);        // I + G H
+    double v = i == j ? 1.0 : 0.0;                                  // its inverse, built alongside
+    bool ok = true;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            wave_lds_order();                                           // earlier reads of sM / sV are done
-            sM[l] = m; sV[l] = v;
-            wave_lds_order();
-            int p = c;                                                  // the largest |M[r][c]|, r >= c
-            double best = fabs(sM[4 * c + c]);
+    for (int c = 0; c < 4; ++c) {
+        wave_lds_order();                                           // earlier reads of sM / sV are done
+        sM[l] = m; sV[l] = v;
+        wave_lds_order();
+        int p = c;                                                  // the largest |M[r][c]|, r >= c
+        double best = fabs(sM[4 * c + c]);
 #pragma unroll
-            for (int r = c + 1; r < 4; ++r) {
-                const double t = fabs(sM[4 * r + c]);
-                p = t > best ? r : p;
-                best = t > best ? t : best;
-            }
-            const int row = i == c ? p : (i == p ? c : i);            // this lane's row after swapping rows c, p
-            const double piv = sM[4 * p + c];
-            ok &= (piv != 0.0) & (fabs(piv) <= 1.7976931348623157e308);
-            const double ip = 1.0 / piv;
-            const double mm = sM[4 * row + j], vv = sV[4 * row + j];
-            const double f = sM[4 * row + c];
-            const double mc = sM[4 * p + j] * ip, vc = sV[4 * p + j] * ip;
-            m = i == c ? mc : fma(-f, mc, mm);
-            v = i == c ? vc : fma(-f, vc, vv);
+        for (int r = c + 1; r < 4; ++r) {
+            const double t = fabs(sM[4 * r + c]);
+            p = t > best ? r : p;
+            best = t > best ? t : best;
         }
-        wave_lds_order();
-        sW[l] = v;
-        wave_lds_order();
-        const double wa = dot_xy(sW, sA, i, j), wg = dot_xy(sW, sG, i, j);
-        sM[l] = wa; sV[l] = wg;                                         // W A, W G
-        wave_lds_order();
-        const double awg = dot_xy(sA, sV, i, j), hwa = dot_xy(sH, sM, i, j), awa = dot_xy(sA, sM, i, j);
-        sT[l] = awg; sU[l] = hwa;
-        wave_lds_order();
-        const double gn = g + dot_xyt(sT, sA, i, j);                   // G + A W G A'
-        const double hn = hh + dot_xty(sA, sU, i, j);                  // H + A' H W A
-        const bool bad = !ok || !(fabs(hn) <= 1.7976931348623157e308);
-        const double d = grp16_max(fabs(hn - hh)), hm = grp16_max(fabs(hn));
-        a = awa; g = gn; hh = hn;
-        if (__any(bad)) return 0;
-        if (d <= 1e-15 * hm) {
-            *P = hh;
-            return step;
-        }
-        wave_lds_order();                                               // reads of this step before the next writes
+        const int row = i == c ? p : (i == p ? c : i);            // this lane's row after swapping rows c, p
+        const double piv = sM[4 * p + c];
+        ok &= (piv != 0.0) & (fabs(piv) <= 1.7976931348623157e308);
+        const double ip = 1.0 / piv;
+        const double mm = sM[4 * row + j], vv = sV[4 * row + j];
+        const double f = sM[4 * row + c];
+        const double mc = sM[4 * p + j] * ip, vc = sV[4 * p + j] * ip;
+        m = i == c ? mc : fma(-f, mc, mm);
+        v = i == c ? vc : fma(-f, vc, vv);
     }
-    return 0;
+    wave_lds_order();
+    sW[l] = v;
+    wave_lds_order();
+    const double wa = dot_xy(sW, sA, i, j), wg = dot_xy(sW, sG, i, j);
+    sM[l] = wa; sV[l] = wg;                                         // W A, W G
+    wave_lds_order();
+    const double awg = dot_xy(sA, sV, i, j), hwa = dot_xy(sH, sM, i, j), awa = dot_xy(sA, sM, i, j);
+    sT[l] = awg; sU[l] = hwa;
+    wave_lds_order();
+    const double gn = g + dot_xyt(sT, sA, i, j);                   // G + A W G A'
+    const double hn = hh + dot_xty(sA, sU, i, j);                  // H + A' H W A
+    const bool bad = !ok || !(fabs(hn) <= 1.7976931348623157e308);
+    a = awa; g = gn; hh = hn;
+    return !__any(bad);
 }
 
 // Workgroup = 4 windows (16 lanes each).  1) every stage the 4 windows use, discretised, into LDS (one lane per
-// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad by doubling (dare_sda16; the
-// reference's fixed point if it does not settle), in every workgroup (the same bits everywhere: no grid-wide
-// dependency);  3) each window's recursion from P = P_inf over stages
+// stage), and the pad (A_f, B_f) at x_f, u_f;  2) compute_P_inf (:144-165) on the pad (doubling jumps, then the
+// reference's loop to its stop iterate), in every workgroup (the same bits everywhere: no grid-wide dependency);  3) each window's recursion from P = P_inf over stages
 // w+L-2 .. w;  its first gain is the QP's solution u0 = K x0 at control step w.
 __global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restrict__ x_ref,
                                                   const double* __restrict__ u_ref, int S,
@@ -387,25 +381,34 @@ __global__ __launch_bounds__(64) void k_mpc_gains(Dyn m, const double* __restric
         }
     }
     __syncthreads();
-    // compute_P_inf on the pad stage: by doubling on every 16-lane group (dare_sda16), the same bits everywhere
+    // compute_P_inf (:144-165) on the pad stage, the same bits in every group: doubling jumps while the map still
+    // moves the iterate by >= tol, then the reference's loop and test from the last such iterate (see sda16_step)
     __shared__ double sm[4][128];
     const MapLane c = map_lane(i, j, m.h, Q, R);
+    const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2, fb3 = pad.b3;
     double P, K0j, K1j;
-    const int steps = dare_sda16(m.h, pad, Q, R, i, j, sm[g], &P);
-    int it;                                               // doublings (> 0), or -(fixed-point iterations)
-    if (steps > 0) {
-        it = steps;
-    } else {   // the doubling did not settle (not a stabilisable pad): the reference's fixed point, from P = Q
-        const double fa2j = pad.a2[j], fa3j = pad.a3[j], fa2i = pad.a2[i], fa3i = pad.a3[i], fb2 = pad.b2,
-                     fb3 = pad.b3;
-        P = c.Qij;
-        it = -(max_iter + 1);                             // the tolerance was never met
-        for (int n = 0; n < max_iter; ++n) {
-            const double nP = riccati_map_lane(P, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
-            const bool conv = __all(fabs(nP - P) < tol);  // np.abs(P - P_prev).max() < tol (a NaN entry fails)
-            P = nP;
-            if (conv) { it = -(n + 1); break; }
+    double Pst = c.Qij;                                   // P_{n0}: the loop below resumes from it
+    int n0 = 0;
+    {
+        double da, dg, dh;
+        sda16_init(m.h, pad, Q, R, i, j, da, dg, dh);
+        for (int s = 1; s <= kSdaMaxSteps; ++s) {
+            if (!sda16_step(i, j, sm[g], da, dg, dh)) break;      // (not a stabilisable pad: the loop from P_{n0})
+            const int idx = (1 << s) - 1;                          // dh = P_idx
+            if (idx >= max_iter) break;                            // the reference never gets past max_iter maps
+            const double nP = riccati_map_lane(dh, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
+            if (__all(fabs(nP - dh) < tol)) break;                 // the reference stops at or before map idx + 1
+            Pst = dh;
+            n0 = idx;
         }
+    }
+    P = Pst;
+    int it = max_iter + 1;                                // the reference's count; max_iter + 1: never converged
+    for (int n = n0; n < max_iter; ++n) {
+        const double nP = riccati_map_lane(P, c, fa2j, fa3j, fa2i, fa3i, fb2, fb3, K0j, K1j);
+        const bool conv = __all(fabs(nP - P) < tol);      // np.abs(P - P_prev).max() < tol (a NaN entry fails)
+        P = nP;
+        if (conv) { it = n + 1; break; }
     }
     if (blockIdx.x == 0 && ln < 16) {
         QT_out[ln] = P;

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 14
+#define GYM_ABI_VERSION 15
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -332,11 +332,12 @@ int gym_dare_fixed_point(const double* A, const double* B, const double Q[16], c
  * (x_ref (N,4), u_ref (N-1,2) [device], S = N-1 stages) and of the pad (A_f, B_f) at x_f (4), u_f (2) [device];
  * Q_T = compute_P_inf(A_f, B_f, Q, R) (max_iter, tol as :144-165); the first gain of windows 0..nwin-1 of length
  * L = T_pred (stage index >= S -> pad).  Replaces gym_dare_fixed_point + gym_tv_lqr_gains(discretize, !all_gains)
- * on host-side Jacobians.  Q_T is computed by doubling (the structure-preserving doubling algorithm: the limit the
- * reference's fixed point approaches, ~10 doublings instead of ~434 dependent maps; within ~1e-12 relative of the
- * reference's stopping point on the cfg 5 pad); if the doubling does not settle, by the reference's fixed point
- * (max_iter, tol).  Outputs [device]: K_out (nwin,2,4), QT_out (4,4), iters_out (1) = the doublings (> 0), or
- * -(the fixed point's iterations as gym_dare_fixed_point counts them).  Q, R [host].  2 <= L <= 254. */
+ * on host-side Jacobians.  Q_T is the reference's stop iterate: doubling steps (the structure-preserving doubling
+ * algorithm, whose k-th iterate is the fixed point's iterate 2^k - 1) jump ahead while one map still moves the
+ * iterate by >= tol, then the reference's loop and test (max|P_next - P| < tol, at most max_iter maps) run from the
+ * last such iterate (cfg 5 pad: 9 doublings + ~180 maps instead of 434 dependent maps).  Outputs [device]: K_out
+ * (nwin,2,4), QT_out (4,4), iters_out (1) = the reference's iteration count as gym_dare_fixed_point reports it
+ * (max_iter + 1: never converged; ABI 15 -- ABI 14 reported doublings).  Q, R [host].  2 <= L <= 254. */
 int gym_mpc_gains(const gym_model* m, const double* x_ref, const double* u_ref, int32_t S, const double* x_f,
                   const double* u_f, const double Q[16], const double R[4], int32_t L, int32_t nwin, int32_t max_iter,
                   double tol, double* K_out, double* QT_out, int32_t* iters_out, void* stream);

@@ -188,3 +188,35 @@ def test_stress_lanes_vs_reference():
         n = min(k_tie, int(ng[j]))
         rel = np.abs(hg[j, :n] - href[:n]) / np.abs(href[:n])
         assert (rel <= COST_REL).all(), (int(lane), k_tie, float(np.nanmax(rel)))
+
+
+def test_stress_tie_lanes_vs_reference():
+    """TIE (3e-12) pinned to the reference itself.  tests/golden/stress_tie_lanes.npz holds the
+    reference's newton_Algorithm run (make_golden_stress_ties.py) on the 58 stress lanes whose GPU / C-oracle divergence
+    has the largest oracle margins (>= 1e-13 at the iteration k where they part, the five above 1e-12 included), each
+    to iteration k, with its per-iteration trial counts and Armijo margins.  The GPU's per-iteration record on the same
+    lanes (serial schedule, bitwise every schedule) must follow the reference's decisions through k, or part from the
+    reference at an iteration where the reference's own margin is below TIE: no GPU decision differs from the
+    reference's except at a tie of the reference's own record."""
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from stress_settle import TIE, gpu_record
+    g = load_golden("stress_tie_lanes")
+    lanes, kdiv = g["lanes"], g["k"]
+    x0 = make_x0(262144, spread=1.5)[lanes]
+    xr, ur = load_refs()
+    _, _, _, tg, _, _ = gpu_record(AcrobotEngine(), x0, xr, ur, max_iters=int(kdiv.max()) + 1)
+    sided, tied = [], []
+    for j, lane in enumerate(lanes):
+        n = int(g["n_iter"][j])                       # the reference ran iterations 0 .. k
+        assert n == int(kdiv[j]) + 1
+        rt, rm = g["trials"][j, :n], g["margin"][j, :n]
+        diff = np.nonzero(tg[j, :n] != rt)[0]
+        if len(diff) == 0:
+            sided.append(int(lane))                   # the GPU takes the reference's decision at k (and before)
+            continue
+        kd = int(diff[0])
+        assert rm[kd] < TIE, (int(lane), kd, int(kdiv[j]), float(rm[kd]), int(tg[j, kd]), int(rt[kd]))
+        tied.append((int(lane), kd))
+    print(f"{len(sided)} lanes take the reference's decisions through k; {len(tied)} part from it at a reference tie")
+    assert len(sided) + len(tied) == len(lanes)

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import rel_l2
+from conftest import ROOT, load_golden, rel_l2
 from oracle import acrobot_np as onp
 from oracle import c_oracle as oc
 
@@ -241,3 +241,30 @@ def test_batch_fixtures_reproduce_on_the_c_oracle(golden, name, spread):
     np.testing.assert_array_equal(o["status"], g["status"][pick])
     np.testing.assert_array_equal(o["n_rollouts"], g["n_rollouts"][pick])
     np.testing.assert_array_equal(o["cost"], g["cost"][pick])
+
+
+def test_c_oracle_parts_from_the_reference_only_at_ties():
+    """The C oracle against the reference's own per-iteration records on the 58 stress tie lanes
+    (tests/golden/stress_tie_lanes.npz, make_golden_stress_ties.py): through each lane's iteration k the oracle
+    evaluates the reference's Armijo trial counts, or first parts from them at an iteration where one of the two
+    records has an Armijo margin below the tie threshold of tests/stress_settle.py (TIE): the restatement takes the
+    reference's decisions except at rounding-level ties."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from bench import load_refs, make_x0
+    from stress_settle import TIE, oracle_record
+    g = load_golden("stress_tie_lanes")
+    lanes, kdiv = g["lanes"], g["k"]
+    x0 = make_x0(262144, spread=1.5)[lanes]
+    xr, ur = load_refs()
+    o = oracle_record(x0, xr, ur, max_iters=int(kdiv.max()) + 1)
+    parted = 0
+    for j, lane in enumerate(lanes):
+        n = int(g["n_iter"][j])
+        rt, rm = g["trials"][j, :n], g["margin"][j, :n]
+        diff = np.nonzero(o["hist_trials"][j, :n] != rt)[0]
+        if len(diff):
+            kd = int(diff[0])
+            parted += 1
+            assert min(rm[kd], o["hist_margin"][j, kd]) < TIE, (int(lane), kd, float(rm[kd]))
+    assert parted >= 30          # most of these lanes are where the oracle alone takes the other side of a tie
