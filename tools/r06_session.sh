@@ -39,6 +39,8 @@ for s in "$@"; do
     p_tccstall) pmc p_tccstall csv TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum TCC_TAG_STALL_sum \
               TCC_BUSY_sum || exit $? ;;
     p_tcc) pmc p_tcc "csv rocpd" TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ_LEVEL || exit $? ;;
+    timeline) step stress_timeline 300 python3 -u tools/stress_timeline.py || exit $? ;;
+    tracest) step trace_stress 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_stress -o run --output-format csv -- python3 -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
