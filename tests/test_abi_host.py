@@ -404,3 +404,33 @@ def test_tracking_feedback_fuses_the_same_product_in_every_rollout():
             for m in muls:
                 regs = re.findall(r"v\[\d+:\d+\]", m)[1:]
                 assert order[1] in regs, (kern, m, order)
+
+
+def test_placement_pool_leases_one_set_per_shape(monkeypatch):
+    """PlacementPool (host logic): a returned set is taken by the next solver of the same key and by no other key;
+    at most one free set per key; free sets beyond MAX_SHARE of the device's memory are dropped oldest first; clear()
+    empties it.  (The GPU side -- the selection inside the first solve, the lease, the < 50 ms second construction --
+    is tests/test_gpu_parity.py::test_placement_selection_is_invisible.)"""
+    import types
+    import torch
+    from gymnast_optimalcontrol_amd.solver import PlacementPool
+    PlacementPool._free.clear()
+    mib = lambda n: ((n * (1 << 20) // 8,),)            # noqa: E731  (one stream of n MiB)
+    monkeypatch.setattr(torch.cuda, "get_device_properties",
+                        lambda i: types.SimpleNamespace(total_memory=100 * (1 << 20)))
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    ka, kb, kc = (0, mib(10)), (0, mib(20)), (0, mib(30))
+    assert PlacementPool.take(ka) is None
+    PlacementPool.put(ka, ["A"], {"chosen": 1})
+    PlacementPool.put(ka, ["A2"], {"chosen": 2})           # one free set per key: the first one stays
+    assert PlacementPool.take(kb) is None
+    assert PlacementPool.take(ka) == (["A"], {"chosen": 1}) and PlacementPool.take(ka) is None
+    PlacementPool.put(ka, ["A"], {})
+    PlacementPool.put(kb, ["B"], {})                       # 30 MiB held, cap 35 MiB
+    assert PlacementPool.held_bytes() == 30 * (1 << 20)
+    PlacementPool.put(kc, ["C"], {})                       # 60 MiB > 35: the oldest (a, then b) dropped
+    assert PlacementPool.take(ka) is None and PlacementPool.take(kb) is None
+    assert PlacementPool.take(kc) == (["C"], {})
+    PlacementPool.put(kc, ["C"], {})
+    PlacementPool.clear()
+    assert PlacementPool.held_bytes() == 0
