@@ -41,6 +41,7 @@ for s in "$@"; do
     p_tcc) pmc p_tcc "csv rocpd" TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ_LEVEL || exit $? ;;
     timeline) step stress_timeline 300 python3 -u tools/stress_timeline.py || exit $? ;;
     tracest) step trace_stress 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_stress -o run --output-format csv -- python3 -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
+    gaps) step trace_gaps 120 python3 -u tools/trace_gaps.py $OUT/trace_cfg3 || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
@@ -50,6 +51,7 @@ for s in "$@"; do
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
     bench20) step bench20 600 python -u bench.py --steps 20 --warmup 2 --extra-legs "" || exit $? ;;
+    driver) step bench_driver 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     trace3) step trace_cfg3 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg3 -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
