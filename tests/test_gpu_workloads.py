@@ -53,6 +53,48 @@ def test_cfg2_full_size_matches_c_oracle():
 
 
 # ----------------------------------------------------------------------------- BASELINE cfg 4 (one GPU)
+def test_cfg4_rank_share_and_pooled_resolve():
+    """One rank's share of BASELINE cfg 4 at N = 8 (bench.py's cfg4_rank_share leg): lanes [0, 131072) of the cfg 4
+    batch, the schedule every rank of that job picks (distributed.schedule_lanes: pipelined, exactly its 512 lanes
+    per CU), with placement selection inside the first solve.  Every lane takes the C oracle's decisions and final
+    cost (the fixture's first 131,072 lanes: make_x0 draws the cfg 4 rows as the cfg 3 ones).  Then the batched
+    newton_Algorithm's one-shot pattern: the solver goes, a new solver of the same shape takes the pooled stream set
+    (no selection) and solves to the same bits."""
+    import gc
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd import distributed as gd
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver, PlacementPool
+    x_ref, u_ref = load_refs()
+    lo, hi = gd.shard_range(1 << 20, 0, 8)
+    x0 = make_x0(1 << 20)[lo:hi]
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, schedule_lanes=gd.schedule_lanes(1 << 20, 8))
+    PlacementPool.clear()
+    s = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **kw)
+    assert s.schedule == "pipelined" and s.placement["state"] == "pending"
+    r = s.solve(x0, 5000, sync_every=4)
+    assert s.placement["state"] == "chosen", s.placement
+    fx = load_golden("headline_oracle")
+    ni, st, nr = (t.cpu().numpy() for t in (r.n_iter, r.status, r.n_rollouts))
+    np.testing.assert_array_equal(ni, fx["n_iter"][lo:hi])
+    np.testing.assert_array_equal(st, fx["status"][lo:hi])
+    np.testing.assert_array_equal(nr, fx["n_rollouts"][lo:hi])
+    rel = np.abs(r.cost.cpu().numpy() - fx["cost"][lo:hi]) / np.abs(fx["cost"][lo:hi])
+    assert rel.max() < 1e-11, rel.max()
+    keep = {k: getattr(r, k)[::97].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")}
+    del r, s
+    gc.collect()
+    s2 = BatchedNewtonSolver(eng, x_ref, u_ref, hi - lo, **kw)
+    assert s2.placement.get("reused"), s2.placement
+    r2 = s2.solve(x0, 5000, sync_every=4)
+    for k, v in keep.items():
+        assert np.array_equal(getattr(r2, k)[::97].cpu().numpy(), v), k
+    del r2, s2
+    gc.collect()
+    PlacementPool.clear()
+
+
 def test_cfg4_global_batch_on_one_gpu():
     """BASELINE cfg 4's whole batch, 1,048,576 lanes (bench.py's strong-scaling workload at N = 1; the pipelined
     schedule), solved to convergence on one GPU, checked through size-independent properties: every lane

@@ -30,6 +30,13 @@ def load_pmc(path):
     if not os.path.exists(path):
         return agg
     rows = list(csv.DictReader(open(path)))
+    # keep the main leg's launches only: per kernel the most common grid size (bench.py's process warm-up runs a small
+    # batch of the same kernels first)
+    grids = defaultdict(lambda: defaultdict(int))
+    for r in rows:
+        grids[short(r["Kernel_Name"])][r.get("Grid_Size", "")] += 1
+    mode = {k: max(g, key=g.get) for k, g in grids.items()}
+    rows = [r for r in rows if r.get("Grid_Size", "") == mode[short(r["Kernel_Name"])]]
     first_phase = None
     for r in rows:
         k = short(r["Kernel_Name"])

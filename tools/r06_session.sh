@@ -42,6 +42,10 @@ for s in "$@"; do
     timeline) step stress_timeline 300 python3 -u tools/stress_timeline.py || exit $? ;;
     tracest) step trace_stress 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_stress -o run --output-format csv -- python3 -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
     gaps) step trace_gaps 120 python3 -u tools/trace_gaps.py $OUT/trace_cfg3 || exit $? ;;
+    fetch) step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_fetch -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
+    write) step pmc_write 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_write -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
+    valu) step pmc_valu 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_nt_" -d $OUT/pmc_valu -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
+    wltest) step pytest_workloads 600 $PYT tests/test_gpu_workloads.py -m gpu -k "rank_share" || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
