@@ -24,7 +24,7 @@ EXPORTS = (
     "gym_riccati_general",
     "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase", "gym_newton_run",
     "gym_newton_tail", "gym_newton_tail_scratch", "gym_newton_cand_scratch", "gym_newton_tail_lds",
-    "gym_newton_finalize", "gym_newton_fill_states", "gym_newton_sigma",
+    "gym_newton_finalize", "gym_newton_fill_states", "gym_placement_probe", "gym_newton_sigma",
     "gym_gamma_sweep", "gym_newton_gamma_sweep",
     "gym_tv_lqr_gains", "gym_dare_fixed_point", "gym_mpc_gains", "gym_lq_forward", "gym_track_rollout", "gym_track_rollout_ex",
     "gym_timing_create", "gym_timing_destroy", "gym_timing_collect",
@@ -32,7 +32,7 @@ EXPORTS = (
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run",
                 "tail")
 
-ABI_VERSION = 15        # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 16        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
@@ -108,6 +108,7 @@ _SIGS = {
     "gym_newton_tail_lds": [_I32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "gym_newton_finalize": [_MP, _WP, _BP, _I32, _P, _P, _P, _P, _P],
     "gym_newton_fill_states": [_MP, _BP, _I32, _P],
+    "gym_placement_probe": [_BP, _I32, _P],
     "gym_newton_sigma": [_MP, _WP, _BP, _P, _P],
     "gym_gamma_sweep": [_MP, _WP, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I32, _P],
     "gym_newton_gamma_sweep": [_MP, _WP, _AP, _BP, _I32, _P, _I32, _P, _P],

@@ -3553,6 +3553,61 @@ int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batc
     return 0;
 }
 
+// Placement probe (gym_placement_probe): the pipelined phase kernel's stream traffic with no arithmetic.  The first
+// half of the workgroups runs the sweep's pattern on lanes [0, Bp/2) (stage T-1 .. 0: read the 2 KiB x_cb block and
+// the 512 B tau2 row of u_cb, write the K1 block and the cg row), the rest the trial's on [Bp/2, Bp) (stage 0 .. T-1:
+// read K1 and cg, write x_cb' at t + 1 and u_cb'), one stage prefetched, non-temporal, four wavefronts per SIMD -- the
+// phase kernel's bytes per launch.  How fast this moves depends on where the driver placed the six streams the same
+// way the phase kernel's speed does (profiles/r06/README.md: 1.84-2.13 ms on eight sets of one process, Pearson
+// 0.87-0.93 against the kernel's own phase times), so a solver ranks candidate stream sets with it in a few ms each.
+// It overwrites the streams (garbage; no NaN traps on the GPU): only before gym_newton_init.
+__global__ __launch_bounds__(BLK, 4) void k_placement_probe(double2* __restrict__ xc, double2* __restrict__ xn,
+                                                            double* __restrict__ uc, double* __restrict__ un,
+                                                            double2* __restrict__ K1, double* __restrict__ cs,
+                                                            int64_t Bp, int T) {
+    const int64_t w = blockIdx.x, j = threadIdx.x;
+    const bool sweep = w < (Bp / BLK) / 2;
+    const int64_t px = w * 2 * BLK + j, pl = w * BLK + j;
+    const int64_t row = 2 * Bp;                  // double2 per knot row of a pair stream; doubles per stage of planes
+    if (sweep) {
+        double2 a = ld_nt(xc + (int64_t)(T - 1) * row + px), b = ld_nt(xc + (int64_t)(T - 1) * row + px + BLK);
+        double c = ld_nt(uc + (int64_t)(T - 1) * row + Bp + pl);
+        for (int t = T - 1; t >= 0; --t) {
+            double2 na = a, nb = b;
+            double nc = c;
+            if (t > 0) {
+                na = ld_nt(xc + (int64_t)(t - 1) * row + px); nb = ld_nt(xc + (int64_t)(t - 1) * row + px + BLK);
+                nc = ld_nt(uc + (int64_t)(t - 1) * row + Bp + pl);
+            }
+            st_nt(K1 + (int64_t)t * row + px, a.x + c, a.y); st_nt(K1 + (int64_t)t * row + px + BLK, b.x, b.y);
+            st_nt(cs + (int64_t)t * row + pl, c);
+            a = na; b = nb; c = nc;
+        }
+    } else {
+        double2 a = ld_nt(K1 + px), b = ld_nt(K1 + px + BLK);
+        double c = ld_nt(cs + pl);
+        for (int t = 0; t < T; ++t) {
+            double2 na = a, nb = b;
+            double nc = c;
+            if (t + 1 < T) {
+                na = ld_nt(K1 + (int64_t)(t + 1) * row + px); nb = ld_nt(K1 + (int64_t)(t + 1) * row + px + BLK);
+                nc = ld_nt(cs + (int64_t)(t + 1) * row + pl);
+            }
+            st_nt(xn + (int64_t)(t + 1) * row + px, a.x + c, a.y); st_nt(xn + (int64_t)(t + 1) * row + px + BLK, b.x, b.y);
+            st_nt(un + (int64_t)t * row + Bp + pl, c);
+            a = na; b = nb; c = nc;
+        }
+    }
+}
+
+int gym_placement_probe(const gym_batch* b, int32_t cb, void* s) {
+    if (bad_batch(b) || cb < 0 || cb > 1 || b->Bp % (2 * BLK) != 0) return GYM_EINVAL;
+    hipLaunchKernelGGL(k_placement_probe, dim3((unsigned)(b->Bp / BLK)), dim3(BLK), 0, (hipStream_t)s,
+                       (double2*)b->x[cb], (double2*)b->x[cb ^ 1], b->u[cb], b->u[cb ^ 1], (double2*)b->K1, b->cs,
+                       b->Bp, b->N - 1);
+    return launch_status();
+}
+
 int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* b, double* sig_out, void* s) {
     if (!m || !w || bad_batch(b) || !sig_out) return GYM_EINVAL;
     hipStream_t st = (hipStream_t)s;

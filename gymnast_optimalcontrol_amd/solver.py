@@ -130,14 +130,18 @@ class BatchedNewtonSolver:
     # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
     # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.
     TAIL_LANES_PER_CU = 4
-    # Placement selection (see PlacementPool and _placement_tick): the phase kernel's speed depends on where its six
-    # stream buffers land (one box: 1.92-2.06 ms per launch for six allocations alive at once, each stable for its
-    # lifetime; profiles/r05/placement/), so a large pipelined solver holds up to this many stream sets during its
-    # first solve, runs blocks of PLACEMENT_BLOCK iterations of that solve on each (the live state copied from set to
-    # set between blocks: the same bits on any set) and keeps the fastest.  Of the 12 sets probed in the round-5 final
-    # lines half were slow (4.10-4.40 ms per probe iteration against 3.95-4.01): four sets leave one selection in 16
-    # on a slow placement, three one in 8 (profiles/r05/final*/bench.log "placement").
-    PLACEMENT_TRIALS = 4
+    # Placement selection (see PlacementPool, _arm_placement and _placement_tick): the phase kernel's speed depends on
+    # where its six stream buffers land (1.89-2.08 ms per launch for sets alive at once in one process, each stable for
+    # its lifetime; profiles/r05/placement/, profiles/r06/README.md).  A large pipelined solver allocates up to
+    # PLACEMENT_CANDIDATES stream sets (as free memory allows), ranks them at construction with the placement probe
+    # (gym_placement_probe: the phase kernel's traffic without arithmetic, ~2 ms a launch; it ranks sets as the kernel
+    # does, Pearson 0.87-0.93), keeps the PLACEMENT_TRIALS best, and races those in its first solve: blocks of
+    # PLACEMENT_BLOCK iterations of that solve on each (the live state copied from set to set between blocks: the same
+    # bits on any set), the fastest kept.  In the zero-arithmetic probe about a third of the sets are fast (1.84-1.86
+    # ms), a third middling (1.95-2.03), the rest slow: eight candidates leave one selection in ~25 without a fast set,
+    # four one in 5 (profiles/r06/layout/).
+    PLACEMENT_CANDIDATES = 8
+    PLACEMENT_TRIALS = 3
     PLACEMENT_BLOCK = 12
     # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
     # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
@@ -392,22 +396,45 @@ class BatchedNewtonSolver:
     # more address-translation misses or any channel imbalance.  Which relative placements are bad is set by where the
     # driver puts the pages, so the solver measures: up to PLACEMENT_TRIALS sets during the first solve, the fastest kept
     # (and pooled for the process's later solvers of the same shape).
-    def _arm_placement(self, trials: int):
-        """Allocate up to ``trials`` - 1 further stream sets (while the free memory allows, beside the lane-major results
-        a solve allocates) for the online selection of the next solve (_placement_tick)."""
+    def _arm_placement(self, trials: int, candidates: int | None = None):
+        """Allocate up to ``candidates`` - 1 further stream sets (while the free memory allows, beside the lane-major
+        results a solve allocates), rank all of them with the placement probe and keep the ``trials`` best for the
+        online selection of the next solve (_placement_tick); the others go back to the device."""
         dev = self.eng.device
+        candidates = max(int(candidates or self.PLACEMENT_CANDIDATES), int(trials))
         set_bytes = 8 * sum(int(np.prod(sh)) for sh in self._stream_shapes)
         B, N, T = self.B, self.N, self.T
         results_bytes = 8 * B * (4 * N + 2 * T + 8 * T + 2 * T)      # finalize's x, u, K, sigma
         free, _ = torch.cuda.mem_get_info(dev)
-        k = min(int(trials), 1 + max(0, int((free - results_bytes - (4 << 30)) // max(set_bytes, 1))))
+        k = min(candidates, 1 + max(0, int((free - results_bytes - (4 << 30)) // max(set_bytes, 1))))
         if k < 2:
             return
         t0 = time.perf_counter()
         sets = [self._streams()] + [[torch.empty(sh, dtype=F64, device=dev) for sh in self._stream_shapes]
                                     for _ in range(k - 1)]
-        self._pl = {"sets": sets, "cur": 0, "attempts": 0, "alloc_s": time.perf_counter() - t0}
-        self.placement = {"trials": k, "state": "pending", "alloc_s": self._pl["alloc_s"]}
+        screen = None
+        if k > trials and self.Bp % 128 == 0:
+            # rank the candidates by the placement probe (two rounds, each set's faster launch), keep the best
+            ms = [float("inf")] * k
+            for r in range(2):
+                for i, st in enumerate(sets):
+                    self._set_streams(st, zero=False)
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                    ev[0].record()
+                    _lib.check(self.eng.lib.gym_placement_probe(C.byref(self.batch), r & 1, self.eng.stream),
+                               "gym_placement_probe")
+                    ev[1].record()
+                    ev[1].synchronize()
+                    ms[i] = min(ms[i], ev[0].elapsed_time(ev[1]))
+            keep = sorted(range(k), key=lambda i: ms[i])[:trials]
+            screen = {"candidates": k, "probe_ms": ms, "kept": keep}
+            sets = [sets[i] for i in keep]
+            torch.cuda.empty_cache()                # the screened-out sets go back to the device
+        self._set_streams(sets[0])                  # K1, cs zeroed (the probe left garbage), as at construction
+        if len(sets) < 2:
+            return
+        self._pl = {"sets": sets, "cur": 0, "attempts": 0, "alloc_s": time.perf_counter() - t0, "screen": screen}
+        self.placement = {"trials": len(sets), "state": "pending", "alloc_s": self._pl["alloc_s"], "screen": screen}
 
     def _placement_start(self):
         """(init) A new solve: the selection schedule restarts from the set in use, in the order c, the others, then
@@ -467,7 +494,7 @@ class BatchedNewtonSolver:
         self.placement = {"trials": len(pl["sets"]), "state": "abandoned" if abandon else "chosen", "chosen": best,
                           "ms_per_iteration": {int(s): v for s, v in sorted(per.items())},
                           "probe_iterations": n * len(pl.get("blocks", [])), "copies": pl.get("copies", 0),
-                          "alloc_s": pl["alloc_s"], "at_iteration": int(self.k)}
+                          "alloc_s": pl["alloc_s"], "at_iteration": int(self.k), "screen": pl.get("screen")}
         self._pl = None
         pl.clear()
         torch.cuda.empty_cache()                    # the unused sets go back to the device, not the process's cache

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 15
+#define GYM_ABI_VERSION 16
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -291,6 +291,11 @@ int gym_newton_finalize(const gym_model* m, const gym_weights* w, const gym_batc
  * res_buf) from its checkpoints and the controls u[buf]: x_{t+1} = RK4(x_t, u_t) from each checkpoint, the
  * trial's arithmetic bit for bit.  Lanes [0, B); a no-op without the flag. */
 int gym_newton_fill_states(const gym_model* m, const gym_batch* bt, int32_t buf, void* stream);
+/* Placement probe: the pipelined phase kernel's stream traffic (gym_newton_phase's bytes per launch: the sweep's
+ * pattern on lanes [0, Bp/2), the trial's on [Bp/2, Bp), buffers cb / cb ^ 1) with no arithmetic, for timing where
+ * the driver placed the six stream buffers (the phase kernel's speed depends on it).  Overwrites x, u, K1
+ * and cs with garbage: call before gym_newton_init.  Bp a multiple of 128. */
+int gym_placement_probe(const gym_batch* bt, int32_t cb, void* stream);
 /* sigma (B,T,2) of each lane's last completed iteration (n_iter - 1): sigma1 by re-running that iteration's
  * sweep (the solver does not stream sigma1; the re-run reproduces it bit for bit), sigma0 recomputed. */
 int gym_newton_sigma(const gym_model* m, const gym_weights* w, const gym_batch* bt, double* sigma_out, void* stream);

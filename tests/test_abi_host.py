@@ -153,10 +153,14 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
                lib.gym_newton_fill_states(R(m), R(b), 0, None),
                lib.gym_newton_finalize(R(m), R(w), R(b), 1, D, D, D, D, None),
                lib.gym_newton_gamma_sweep(R(m), R(w), R(a), R(b), 0, D, 4, D, None),
-               lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 1, D, 1 << 40, 0, 1, None)]
-        assert rcs == [1] * 9, (b.B, b.Bp, b.N, b.flags, rcs)
+               lib.gym_newton_tail(R(m), R(w), R(a), R(b), D, 1, D, 1 << 40, 0, 1, None),
+               lib.gym_placement_probe(R(b), 0, None)]
+        assert rcs == [1] * 10, (b.B, b.Bp, b.N, b.flags, rcs)
     b = batch()
     assert lib.gym_newton_run(R(m), R(w), R(a), R(b), 5, 1, None) == 1                   # k1 < k0
+    # the placement probe (ABI 16): buffer 0 / 1 only, lanes in whole pairs of wavefronts (its halves)
+    assert lib.gym_placement_probe(R(b), 2, None) == 1 and lib.gym_placement_probe(R(b), -1, None) == 1
+    assert lib.gym_placement_probe(R(b), 0, None) == 1                                   # Bp = 64: one wavefront
     need = C.c_int64()
     assert lib.gym_newton_tail_scratch(501, 3, 20, C.byref(need)) == 0 and need.value == 64 * (4 * 501 + 2 * 500)
     assert lib.gym_newton_tail_scratch(501, 3, 65, C.byref(need)) == 1                  # > 64 trials

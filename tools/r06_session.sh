@@ -46,6 +46,12 @@ for s in "$@"; do
     write) step pmc_write 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_" -d $OUT/pmc_write -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
     valu) step pmc_valu 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_nt_" -d $OUT/pmc_valu -o run --output-format csv -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" || exit $? ;;
     wltest) step pytest_workloads 600 $PYT tests/test_gpu_workloads.py -m gpu -k "rank_share" || exit $? ;;
+    l6) step layout6 300 python3 -u tools/layout6_probe.py --out $OUT/l6.json || exit $? ;;
+    l6b) step layout6b 300 python3 -u tools/layout6_probe.py --sep-sets 6 --rec-sets 6 --seconds 0.6 --out $OUT/l6b.json || exit $? ;;
+    l6c) step layout6c 300 python3 -u tools/layout6_probe.py --sep-sets 6 --rec-sets 6 --seconds 0.6 --out $OUT/l6c.json || exit $? ;;
+    lsearch) step layout_search 400 python3 -u tools/layout_search.py --out $OUT/search.json || exit $? ;;
+    pvk) step probe_vs_kernel 300 python3 -u tools/probe_vs_kernel.py --out $OUT/pvk.json || exit $? ;;
+    pvk2) step probe_vs_kernel2 300 python3 -u tools/probe_vs_kernel.py --out $OUT/pvk2.json || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
