@@ -389,13 +389,12 @@ class BatchedNewtonSolver:
         self._set_streams(st, zero=False)
 
     # --- placement selection ---------------------------------------------------------------
-    # Which placements are slow (profiles/r06/placement/): the slowness follows the RELATIVE placement of the streams the
-    # same waves touch in lock step -- on a slow set, replacing either K1 or cs by a fast set's copy makes it fast, while
-    # x0 / x1 / u0 / u1 do not matter, each buffer alone streams at the same rate wherever it lies, and the slow set shows
-    # ~2x the L2's fabric-side write / read-credit stalls and ~25% longer read latency at the same request counts, not
-    # more address-translation misses or any channel imbalance.  Which relative placements are bad is set by where the
-    # driver puts the pages, so the solver measures: up to PLACEMENT_TRIALS sets during the first solve, the fastest kept
-    # (and pooled for the process's later solvers of the same shape).
+    # Why placements differ (profiles/r06/README.md): on a slow set the same fabric requests come back later (+13..24%
+    # read latency, ~2x the L2's DRAM-credit and write stalls; no more translation misses, no channel imbalance), and
+    # the slowness follows how the streams the same waves touch in lock step lie relative to each other in physical
+    # memory; no allocation rule reachable from user space fixes it (contiguous VRAM at 200 layouts, record layouts),
+    # so the solver measures: candidates ranked by the placement probe, the best raced in the first solve, the winner
+    # pooled for the process's later solvers of the same shape.
     def _arm_placement(self, trials: int, candidates: int | None = None):
         """Allocate up to ``candidates`` - 1 further stream sets (while the free memory allows, beside the lane-major
         results a solve allocates), rank all of them with the placement probe and keep the ``trials`` best for the
