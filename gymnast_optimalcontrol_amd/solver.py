@@ -142,6 +142,7 @@ class BatchedNewtonSolver:
     # four one in 5 (profiles/r06/layout/).
     PLACEMENT_CANDIDATES = 8
     PLACEMENT_TRIALS = 3
+    PLACEMENT_MEM_SHARE = 0.45
     PLACEMENT_BLOCK = 12
     # Candidate slots of the post-trial Armijo search (gym_batch.cand_scratch): 32,768 (0.79 GB at T = 500) cover
     # 1,724 backtracking lanes at max_ls = 20; a hard solve's iterations mostly have 0-30 (tools/retry_counts.py).
@@ -404,13 +405,24 @@ class BatchedNewtonSolver:
         set_bytes = 8 * sum(int(np.prod(sh)) for sh in self._stream_shapes)
         B, N, T = self.B, self.N, self.T
         results_bytes = 8 * B * (4 * N + 2 * T + 8 * T + 2 * T)      # finalize's x, u, K, sigma
-        free, _ = torch.cuda.mem_get_info(dev)
-        k = min(candidates, 1 + max(0, int((free - results_bytes - (4 << 30)) // max(set_bytes, 1))))
+        free, total = torch.cuda.mem_get_info(dev)
+        # beside the results a solve allocates, and at most PLACEMENT_MEM_SHARE of the device for the extra sets (so
+        # that processes sharing a GPU leave each other room); an allocation that fails (another process was faster)
+        # just ends the candidate list
+        room = min(free - results_bytes - (4 << 30), self.PLACEMENT_MEM_SHARE * total)
+        k = min(candidates, 1 + max(0, int(room // max(set_bytes, 1))))
         if k < 2:
             return
         t0 = time.perf_counter()
-        sets = [self._streams()] + [[torch.empty(sh, dtype=F64, device=dev) for sh in self._stream_shapes]
-                                    for _ in range(k - 1)]
+        sets = [self._streams()]
+        try:
+            for _ in range(k - 1):
+                sets.append([torch.empty(sh, dtype=F64, device=dev) for sh in self._stream_shapes])
+        except torch.cuda.OutOfMemoryError:
+            torch.cuda.empty_cache()
+        k = len(sets)
+        if k < 2:
+            return
         screen = None
         if k > trials and self.Bp % 128 == 0:
             # rank the candidates by the placement probe (two rounds, each set's faster launch), keep the best

@@ -52,6 +52,8 @@ for s in "$@"; do
     lsearch) step layout_search 400 python3 -u tools/layout_search.py --out $OUT/search.json || exit $? ;;
     pvk) step probe_vs_kernel 300 python3 -u tools/probe_vs_kernel.py --out $OUT/pvk.json || exit $? ;;
     pvk2) step probe_vs_kernel2 300 python3 -u tools/probe_vs_kernel.py --out $OUT/pvk2.json || exit $? ;;
+    greedy) step greedy 300 python3 -u tools/greedy_streams.py --out $OUT/g.json || exit $? ;;
+    greedy2) step greedy2 300 python3 -u tools/greedy_streams.py --out $OUT/g2.json || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
@@ -61,6 +63,8 @@ for s in "$@"; do
     smoke) step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python -u bench.py || exit $? ;;
     bench20) step bench20 600 python -u bench.py --steps 20 --warmup 2 --extra-legs "" || exit $? ;;
+    main20a) step main20a 400 python3 -u bench.py --steps 20 --warmup 5 --no-cpu --extra-legs "" || exit $? ;;
+    main20b) step main20b 400 python3 -u bench.py --steps 20 --warmup 5 --no-cpu --extra-legs "" || exit $? ;;
     driver) step bench_driver 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     trace3) step trace_cfg3 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg3 -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
