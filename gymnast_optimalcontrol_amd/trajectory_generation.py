@@ -370,7 +370,7 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
         solver.iteration()
         status = int(solver.status[0].item())
         sig = lane_sigma()
-        history["sigmas"].append([sig[t].copy() for t in range(Tn)])
+        history["sigmas"].append(list(sig))          # row views of this iteration's own (T,2) array
         history["sigma_norm"].append(float(solver.smax[0].item()))
         if status == _lib.LS_FAILED:
             if verbose:

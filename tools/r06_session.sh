@@ -54,6 +54,7 @@ for s in "$@"; do
     pvk2) step probe_vs_kernel2 300 python3 -u tools/probe_vs_kernel.py --out $OUT/pvk2.json || exit $? ;;
     greedy) step greedy 300 python3 -u tools/greedy_streams.py --out $OUT/g.json || exit $? ;;
     greedy2) step greedy2 300 python3 -u tools/greedy_streams.py --out $OUT/g2.json || exit $? ;;
+    cfg2ab) step cfg2_4waves 300 python3 -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" && step cfg2_1wave 300 python3 -u bench.py --batch 4096 --steps 5 --warmup 1 --no-cpu --extra-legs "" --split-waves off || exit $? ;;
     first) step first_solve 300 python3 -u tools/first_solve.py --out $OUT/first.json || exit $? ;;
     tietest) step pytest_ties 300 $PYT tests/test_gpu_stress.py -m gpu -k tie_lanes -s || exit $? ;;
     ttest) step pytest_tracking 300 $PYT tests/test_tracking.py -m gpu || exit $? ;;
