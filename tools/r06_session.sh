@@ -68,6 +68,10 @@ for s in "$@"; do
     main20b) step main20b 400 python3 -u bench.py --steps 20 --warmup 5 --no-cpu --extra-legs "" || exit $? ;;
     driver) step bench_driver 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     trace3) step trace_cfg3 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg3 -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
+    two) GYM_DIST_BACKEND=gloo step bench_2rank 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+           --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 || exit $? ;;
+    four) GYM_DIST_BACKEND=gloo step bench_4rank 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+           --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
