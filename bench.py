@@ -758,6 +758,7 @@ def main():
         out["roofline"].update({k: v for k, v in roof.items() if k not in out["roofline"]})
         out["kernels"] = kern
     out["schedule"] = main_leg.schedule()
+    out["phase_kernel"] = sv.phase_kind()
     out["setup"] = dict(main_leg.setup_record(), cold_start_s=cold_s, note=(
         "setup_s: solver construction (buffers, and the extra stream sets of placement selection); first_solve_s: the "
         "first solve of the solver (warm-up; placement selection runs inside it: blocks of 12 iterations of that solve "
@@ -865,6 +866,7 @@ def main():
         out["cfg4_rank_share"] = {
             "value": leg.value, "unit": "Newton iterations/s", "lanes": leg.solver.B, "steps": a.extra_steps,
             "warmup": 1, "ms_per_step": 1e3 * leg.elapsed / a.extra_steps, "schedule": leg.schedule(),
+            "phase_kernel": leg.solver.phase_kind(),
             "lane_iterations_per_step": leg.lane_its_all // a.extra_steps,
             "roofline": None if rsh is None else {k: rsh[k] for k in ("kernel", "achieved", "peak", "unit", "frac")},
             "setup": leg.setup_record(),

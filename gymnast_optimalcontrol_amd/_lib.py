@@ -22,7 +22,8 @@ EXPORTS = (
     "gym_pack_lanes", "gym_unpack_lanes", "gym_unpack_gains",
     "gym_rollout_open_loop", "gym_closed_loop", "gym_total_cost", "gym_backward_sweep", "gym_linearize",
     "gym_riccati_general",
-    "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase", "gym_newton_run",
+    "gym_newton_init", "gym_newton_iteration", "gym_newton_pipeline_split", "gym_newton_phase", "gym_newton_phase_kind",
+    "gym_newton_run",
     "gym_newton_tail", "gym_newton_tail_scratch", "gym_newton_cand_scratch", "gym_newton_tail_lds",
     "gym_newton_finalize", "gym_newton_fill_states", "gym_placement_probe", "gym_newton_sigma",
     "gym_gamma_sweep", "gym_newton_gamma_sweep",
@@ -32,7 +33,7 @@ EXPORTS = (
 KERNEL_KINDS = ("backward", "trial", "candidates", "retry", "stats", "phase_odd", "phase_even", "sigma", "run",
                 "tail")
 
-ABI_VERSION = 16        # GYM_ABI_VERSION of the header this binding mirrors
+ABI_VERSION = 17        # GYM_ABI_VERSION of the header this binding mirrors
 MAX_BP = 1 << 26         # GYM_MAX_BP
 FLAG_U0_ZERO = 1         # GYM_FLAG_U0_ZERO
 FLAG_X_CKPT = 2          # GYM_FLAG_X_CKPT
@@ -100,6 +101,7 @@ _SIGS = {
     "gym_newton_init": [_MP, _WP, _P, _BP, _P],
     "gym_newton_iteration": [_MP, _WP, _AP, _BP, _I32, _P],
     "gym_newton_pipeline_split": [_BP, C.POINTER(C.c_int64)],
+    "gym_newton_phase_kind": [_BP, C.POINTER(C.c_int32)],
     "gym_newton_phase": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_run": [_MP, _WP, _AP, _BP, _I32, _I32, _P],
     "gym_newton_tail": [_MP, _WP, _AP, _BP, _P, _I32, _P, _I64, _I32, _I32, _P],

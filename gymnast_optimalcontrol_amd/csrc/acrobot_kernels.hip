@@ -286,7 +286,7 @@ __device__ __forceinline__ double trial_u1_sig(double2 k0, double2 k1, double cg
     return __builtin_fma(dg, s1, cg + kx);
 }
 
-template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT, bool BAND = true>
+template <bool WRITE, bool U0Z, bool SIG, bool CK = false, int CP = kNT, bool BAND = true, int PD = 1>
 __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const double* __restrict__ u,
                                                 const double2* __restrict__ K1, const double* __restrict__ cs,
                                                 const double* __restrict__ xr, const double* __restrict__ ur,
@@ -342,14 +342,36 @@ __device__ __forceinline__ double rollout_cform(const Dyn& m, const KW& w, const
             bst2(rX, o2, WROW, n2, n3);
         }
     };
-    TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
-    fetch(pre, 0);
-    pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
-    prio_start<BAND ? 1 : PRIO_NONE>();
-    for (int t = 0; t < T; ++t) {
-        const TrialStage q = pre;
-        fetch(pre, t + 1 < T ? t + 1 : t);   // unconditional (the last stage's copy unused): no phi, no copies
-        body(q, t);
+    if constexpr (PD == 1) {
+        TrialStage pre;   // software prefetch of stage t+1's streams while stage t computes
+        fetch(pre, 0);
+        pin(pre.k0); pin(pre.k1); pin(pre.cg); pin(pre.s1); pin(pre.u0);
+        prio_start<BAND ? 1 : PRIO_NONE>();
+        for (int t = 0; t < T; ++t) {
+            const TrialStage q = pre;
+            fetch(pre, t + 1 < T ? t + 1 : t);   // unconditional (the last stage's copy unused): no phi, no copies
+            body(q, t);
+        }
+    } else {
+        // prefetch distance 2 (few wavefronts per SIMD: two stages of loads in flight behind each stage's compute):
+        // three register sets in rotation, unrolled by 3 so that no set is copied (a copy waits for its load)
+        static_assert(PD == 2, "prefetch distance 1 or 2");
+        auto clampT = [&](int v) { return __builtin_amdgcn_readfirstlane(v < T ? v : T - 1); };
+        TrialStage s0, s1, s2;
+        fetch(s0, 0);
+        fetch(s1, clampT(1));
+        prio_start<BAND ? 1 : PRIO_NONE>();
+        int t = 0;
+        for (; t + 3 <= T; t += 3) {
+            fetch(s2, clampT(t + 2));
+            body(s0, t);
+            fetch(s0, clampT(t + 3));
+            body(s1, t + 1);
+            fetch(s1, clampT(t + 4));
+            body(s2, t + 2);
+        }
+        if (t < T) body(s0, t);
+        if (t + 1 < T) body(s1, t + 1);
     }
     return J + xcost(w.QT, n0, n1, n2, n3, xr + 4 * T);
 }
@@ -553,6 +575,12 @@ __device__ __forceinline__ void backward_lane(const Dyn& m, const KW& w, const d
     smax_out = S.smax;
 }
 
+// Streams of one sweep stage (x_t pairs, u_t planes), prefetched into registers ahead of the stage.
+struct SweepStage {
+    double2 xa, xb;
+    double u0, u1;
+};
+
 // What a solver sweep stores: K row 1 + cg (every iteration), sigma1 only (re-run for the trials 2..20 and
 // the final sigma), or all three (gamma sweeps).
 enum SweepOut { OUT_SOLVER = 0, OUT_SIGMA = 1, OUT_ALL = 2 };
@@ -582,7 +610,7 @@ __device__ __forceinline__ void store_stage(const char* Kb, const char* Cb, int 
 // Solver sweep of one lane: writes K row 1 and cg = (u1 - K1 x) + gamma0 sigma1 (and / or sigma1, OUT),
 // prefetching stage t-1's streams while stage t computes.  U0Z: the tau1 channel is identically zero
 // (u0 = ur0 = 0, GYM_FLAG_U0_ZERO) and its plane is not read.
-template <bool U0Z, int OUT, bool BAND = true>
+template <bool U0Z, int OUT, bool BAND = true, int PD = 1>
 __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
                                                      const double2* __restrict__ x, const double* __restrict__ u,
                                                      const double* __restrict__ xr, const double* __restrict__ ur,
@@ -598,6 +626,44 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
     const char* Cb = reinterpret_cast<const char*>(cs);
     Sweep<false> S(w, x[wix(T, 0, 2, l, Bp)], x[wix(T, 1, 2, l, Bp)], xr + 4 * T);
     const gym::PolyRegs pk = gym::poly_vgprs();
+    if constexpr (PD == 2) {
+        // prefetch distance 2: three stream sets in rotation, unrolled by 3 (see rollout_cform)
+        auto fetch = [&](SweepStage& q, int t) {
+            const int tp = __builtin_amdgcn_readfirstlane(t > 0 ? t : 0);
+            const auto rX = rsrc(Xb + (int64_t)tp * (2 * (int64_t)row));
+            const auto rU = rsrc(Ub + (int64_t)tp * row);
+            q.xa = bld2(rX, o2, 0);
+            q.xb = bld2(rX, o2, WROW);
+            q.u0 = U0Z ? 0.0 : bld1(rU, o1, 0);
+            q.u1 = bld1(rU, o1, plane);
+        };
+        auto body = [&](const SweepStage& q, int t) {
+            prio_band<BAND ? 0 : PRIO_NONE>(T - 1 - t, T);
+            double k0, k1, k2, k3, s0, s1;
+            const KArgs ka = kernarg_consts();
+            S.template step<U0Z>(ka.m, ka.w, q.xa, q.xb, q.u0, q.u1, xr + 4 * t, ur + 2 * t, k0, k1, k2, k3, s0, s1,
+                                 pk);
+            store_stage<OUT>(Kb, Cb, t, row, plane, o2, o1, q.xa, q.xb, q.u1, g0, k0, k1, k2, k3, s1);
+        };
+        SweepStage s0, s1, s2;
+        fetch(s0, T - 1);
+        fetch(s1, T - 2);
+        prio_start<BAND ? 0 : PRIO_NONE>();
+        int t = T - 1;
+        for (; t >= 2; t -= 3) {
+            fetch(s2, t - 2);
+            body(s0, t);
+            fetch(s0, t - 3);
+            body(s1, t - 1);
+            fetch(s1, t - 4);
+            body(s2, t - 2);
+        }
+        if (t >= 0) body(s0, t);
+        if (t >= 1) body(s1, t - 1);
+        dJ_out = S.dJ;
+        smax_out = S.smax;
+        return;
+    }
     double2 pa, pb;
     double pu0 = 0.0, pu1;
     {
@@ -635,10 +701,6 @@ __device__ __forceinline__ void backward_solver_lane(const Dyn& m, const KW& w,
 // registers one stage early: prefetch distance 2, three stream sets and two Jacobians in rotation (unrolled by
 // 6, so that no set is copied -- a copy of a loading register waits for its load).  Same per-stage arithmetic
 // as backward_solver_lane (step = jacobian + step_j): the same bits.
-struct SweepStage {
-    double2 xa, xb;
-    double u0, u1;
-};
 template <bool U0Z, int OUT>
 __device__ __forceinline__ void backward_solver_lane_ilp(const Dyn& m, const KW& w,
                                                          const double2* __restrict__ x, const double* __restrict__ u,
@@ -1408,8 +1470,13 @@ __device__ __forceinline__ pargs_t phase_args() {
     return (pargs_t)p;
 }
 
-template <bool U0Z, bool CK, bool RL = false>
-__global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
+// LO: the phase for at most two wavefronts per SIMD (gym_newton_phase's choice by the launch's size), compiled for
+// two (up to 256 VGPRs) with both stage loops prefetching two stages ahead (three stream sets in rotation): with
+// half the headline's waves a stage's loads must be issued further ahead to keep as many bytes in flight.  The same
+// arithmetic in the same order (the same bits; tests/test_gpu_workloads.py).  Not with CK.
+template <bool U0Z, bool CK, bool RL = false, bool LO = false>
+__global__ __launch_bounds__(BLK, LO ? 2 : 4) void k_nt_phase(PhaseArgs args) {
+    constexpr int PD = LO && !CK ? 2 : 1;
     GYM_CK_LDS(CK, U0Z);
     if ((int)blockIdx.x < args.nb_b) {
         const int64_t l = args.rb.lo + (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -1423,8 +1490,9 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
                 backward_solver_lane_ck<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1, R->cs,
                                                          R->a.gamma0, ck_lds, l, R->Bp, R->N, d, s);
             else
-                backward_solver_lane<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1, R->cs,
-                                                      R->a.gamma0, l, R->Bp, R->N, d, s);
+                backward_solver_lane<U0Z, OUT_SOLVER, true, PD>(R->m, R->w, R->xb_in, R->ub_in, xr, ur,
+                                                                         R->K1, R->cs, R->a.gamma0, l, R->Bp, R->N,
+                                                                         d, s);
         }
         const pargs_t Q = phase_args();
         Q->dJ[l] = d;
@@ -1437,7 +1505,7 @@ __global__ __launch_bounds__(BLK, 4) void k_nt_phase(PhaseArgs args) {
         {   // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass)
             const pargs_t R = phase_args();
             const double2 xa = R->io.x[wix(0, 0, 2, l, R->Bp)], xb = R->io.x[wix(0, 1, 2, l, R->Bp)];
-            Jn = rollout_cform<true, U0Z, false, CK>(R->m, R->w, R->io.u, R->K1, R->cs,
+            Jn = rollout_cform<true, U0Z, false, CK, kNT, true, PD>(R->m, R->w, R->io.u, R->K1, R->cs,
                                                      lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N),
                                                      lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1)), R->io.xn,
                                                      R->io.un, R->a.gamma0, R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y,
@@ -3042,6 +3110,12 @@ struct TimedLaunch {  // records a start/stop event pair around one launch: a po
                                                                           : kern<false, false, true>)           \
                                       : SOLVER_SEL(b, kern))
 #define RUN_SEL(b, kern) CAND_SEL(b, kern)   // the persistent kernels: <U0Z, RL>
+// the low-occupancy phase kernel (k_nt_phase<..., LO = true>; never with X_CKPT)
+#define PHASE_LO_SEL(b)                                                                                          \
+    (((b)->flags & GYM_FLAG_REF_LANE)                                                                            \
+         ? (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, true, true> : k_nt_phase<false, false, true, true>) \
+         : (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, false, true>                               \
+                                             : k_nt_phase<false, false, false, true>))
 #define CAND_SEL(b, kern)                                                                                        \
     (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, true> : kern<false, true>) \
                                       : (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false> : kern<false, false>))
@@ -3341,6 +3415,37 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
     return launch_status();
 }
 
+// compute units of the current device (cached per device index; 0 if the query fails)
+static int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+// The phase kernel for a launch of `waves` wavefronts: the low-occupancy build (k_nt_phase<..., LO>) when the
+// launch fills the SIMDs with between LO_MIN_EIGHTHS/8 and two wavefronts each (profiles/r06/README.md "pd2":
+// same-buffer A/B over batch sizes), the four-wavefront build otherwise.
+constexpr int LO_MIN_EIGHTHS = 14;
+static bool phase_low_occupancy(const gym_batch* b, int64_t waves) {
+    if (b->flags & GYM_FLAG_X_CKPT) return false;
+    const int64_t simds = 4 * (int64_t)device_cus();
+    return simds > 0 && 8 * waves > LO_MIN_EIGHTHS * simds && waves <= 2 * simds;
+}
+
+int gym_newton_phase_kind(const gym_batch* b, int32_t* low_out) {
+    if (bad_batch(b) || !low_out) return GYM_EINVAL;
+    int64_t Bh;
+    gym_newton_pipeline_split(b, &Bh);
+    const int64_t waves = (Bh + BLK - 1) / BLK + (b->B - Bh + BLK - 1) / BLK;
+    *low_out = phase_low_occupancy(b, waves) ? 1 : 0;
+    return 0;
+}
+
 int gym_newton_pipeline_split(const gym_batch* b, int64_t* Bh) {
     if (!b || !Bh || b->B <= 0) return GYM_EINVAL;
     int64_t h = ((b->B + 1) / 2 + 63) / 64 * 64;
@@ -3380,7 +3485,8 @@ int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo*
         pa.retry_list = b->retry_list; pa.counter = b->counters + ht;
         pa.hist_cost = hist ? b->hist_cost : nullptr; pa.hist_smax = hist ? b->hist_smax : nullptr;
         pa.rb = rb; pa.rt = rt; pa.Bp = b->Bp; pa.N = b->N; pa.kb = kb; pa.nb_b = nb_b; pa.pad = 0;
-        hipLaunchKernelGGL(SERIAL_SEL(b, k_nt_phase), dim3(nb_b + nb_t), dim3(BLK), 0, st, pa);
+        hipLaunchKernelGGL(phase_low_occupancy(b, nb_b + nb_t) ? PHASE_LO_SEL(b) : SERIAL_SEL(b, k_nt_phase),
+                           dim3(nb_b + nb_t), dim3(BLK), 0, st, pa);
     }
     if (p >= 1)  // the trial half's retries and statistics; H1 closes the iteration: total = H0 + H1
         launch_post_trial(m, w, a, b, c, io, rt, b->counters + ht, b->stats + 8 + 8 * ht,

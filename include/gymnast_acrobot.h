@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GYM_ABI_VERSION 16
+#define GYM_ABI_VERSION 17
 #define GYM_MAX_BP (1LL << 26) /* lane stride limit: stream offsets are 32-bit inside one stage      */
 
 /* gym_batch.flags */
@@ -254,6 +254,11 @@ int gym_newton_iteration(const gym_model* m, const gym_weights* w, const gym_arm
 int gym_newton_pipeline_split(const gym_batch* bt, int64_t* Bh);
 int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t p,
                      int32_t do_backward, void* stream);
+/* Which build of the phase kernel gym_newton_phase launches for this batch's full phases on the current device:
+ * *low_out = 1 for the low-occupancy build (more than 7/8 and at most two wavefronts per SIMD, no X_CKPT: compiled
+ * for two wavefronts, its stage loops prefetching two stages ahead), 0 for the four-wavefront build.  Both give the
+ * same bits; this reports the choice (tests, the bench line).  ABI 17. */
+int gym_newton_phase_kind(const gym_batch* bt, int32_t* low_out);
 /* Persistent schedule: ONE launch in which every lane still ACTIVE runs its own outer iterations k0 .. k1-1 back to
  * back (newton_Algorithm :329-396 per lane: sweep, Armijo trial 1, and for a lane that rejects it the sigma1 re-run
  * and trials 2..max_ls in sequence), stopping at convergence or LS failure; then the statistics of iteration k1-1

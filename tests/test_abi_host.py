@@ -161,6 +161,12 @@ def test_batch_entry_points_reject_bad_sizes_and_flags():
     # the placement probe (ABI 16): buffer 0 / 1 only, lanes in whole pairs of wavefronts (its halves)
     assert lib.gym_placement_probe(R(b), 2, None) == 1 and lib.gym_placement_probe(R(b), -1, None) == 1
     assert lib.gym_placement_probe(R(b), 0, None) == 1                                   # Bp = 64: one wavefront
+    # which phase-kernel build (ABI 17): refuses a missing output and a malformed batch before any device query
+    kind = C.c_int32(-1)
+    assert lib.gym_newton_phase_kind(R(b), None) == 1 and lib.gym_newton_phase_kind(None, C.byref(kind)) == 1
+    bad = batch()
+    bad.Bp = 100
+    assert lib.gym_newton_phase_kind(R(bad), C.byref(kind)) == 1 and kind.value == -1
     need = C.c_int64()
     assert lib.gym_newton_tail_scratch(501, 3, 20, C.byref(need)) == 0 and need.value == 64 * (4 * 501 + 2 * 500)
     assert lib.gym_newton_tail_scratch(501, 3, 65, C.byref(need)) == 1                  # > 64 trials

@@ -95,6 +95,40 @@ def test_cfg4_rank_share_and_pooled_resolve():
     PlacementPool.clear()
 
 
+def test_low_occupancy_phase_kernel_is_bitwise_the_four_wavefront_one():
+    """gym_newton_phase picks its low-occupancy build (compiled for two wavefronts per SIMD, both stage loops
+    prefetching two stages ahead) for batches of more than 7/8 and at most two wavefronts per SIMD, e.g. the
+    131,072 lanes of one rank's cfg 4 share, and its four-wavefront build for the headline 262,144.  Same arithmetic
+    in the same order: lanes [0, 131072) of the headline solve and the 131,072-lane solve agree bit for bit in every
+    output (iteration counts, statuses and rollouts on every lane; x, u, K, sigma and cost on every 97th lane)."""
+    import gc
+    import torch
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    x_ref, u_ref = load_refs()
+    eng = AcrobotEngine()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    x0 = make_x0(262144)
+    kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, placement_trials=1)
+    out = {}
+    for B in (131072, 262144):
+        s = BatchedNewtonSolver(eng, x_ref, u_ref, B, **kw)
+        assert s.schedule == "pipelined"
+        waves, simds = B // 64, 4 * cus
+        want = "low-occupancy" if 8 * waves > 14 * simds and waves <= 2 * simds else "four-wavefront"
+        assert s.phase_kind() == want, (B, cus, s.phase_kind())
+        if cus == 256:                           # MI355X: the rank share on the low-occupancy build, the headline not
+            assert want == ("low-occupancy" if B == 131072 else "four-wavefront")
+        r = s.solve(x0[:B], 5000, sync_every=4)
+        out[B] = {k: getattr(r, k)[:131072].cpu().numpy() for k in ("n_iter", "status", "n_rollouts")}
+        out[B].update({k: getattr(r, k)[:131072:97].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")})
+        del r, s
+        gc.collect()
+    for k, v in out[262144].items():
+        assert np.array_equal(out[131072][k], v), k
+
+
 def test_cfg4_global_batch_on_one_gpu():
     """BASELINE cfg 4's whole batch, 1,048,576 lanes (bench.py's strong-scaling workload at N = 1; the pipelined
     schedule), solved to convergence on one GPU, checked through size-independent properties: every lane

@@ -17,6 +17,7 @@ step() {  # step <name> <seconds> <cmd...>
 }
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
 PP="python3 -u tools/placement_pmc.py --sets ${PSETS:-6}"
+LIB=gymnast_optimalcontrol_amd/libgymnast_acrobot.so
 pmc() {  # pmc <name> <format> <counters...>: one rocprofv3 pass over tools/placement_pmc.py, then its summary
   local name=$1 fmt=$2; shift 2
   step $name 300 rocprofv3 --pmc "$@" --kernel-include-regex k_nt_phase -d $OUT/$name -o run --output-format $fmt \
@@ -72,6 +73,17 @@ for s in "$@"; do
            --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 || exit $? ;;
     four) GYM_DIST_BACKEND=gloo step bench_4rank 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
            --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 || exit $? ;;
+    pd2cmp) GYM_ALLOW_FOREIGN_BUILD=1 step pd2_compare 300 python3 -u tools/compare_libs.py $LIB build_ab/libpd2.so --batch 131072 --iters 6 \
+              --schedule pipelined || exit $? ;;
+    pd2ab) for b in ${PD2_BATCHES:-131072 98304 196608 262144}; do
+             GYM_ALLOW_FOREIGN_BUILD=1 step pd2_ab_$b 400 python3 -u tools/ab_bench.py --batch $b --rounds 3 $LIB:pipe build_ab/libpd2.so:pipe \
+               || exit $?; done ;;
+    spread) for b in ${SP_BATCHES:-114688 131072 163840 196608 262144}; do
+             GYM_ALLOW_FOREIGN_BUILD=1 step spread_ab_$b 400 python3 -u tools/ab_bench.py --batch $b --rounds 3 \
+               build_ab/libA.so:pipe build_ab/libB.so:pipe build_ab/libC.so:pipe build_ab/libD.so:pipe || exit $?; done ;;
+    lotest) step pytest_lo 600 $PYT tests/test_gpu_workloads.py -m gpu -k "low_occupancy or rank_share" || exit $? ;;
+    sharebench) step bench_share 600 python3 -u bench.py --steps 5 --warmup 2 --no-cpu --extra-legs cfg4share,cfg4 \
+                  || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
