@@ -3110,7 +3110,7 @@ struct TimedLaunch {  // records a start/stop event pair around one launch: a po
                                                                           : kern<false, false, true>)           \
                                       : SOLVER_SEL(b, kern))
 #define RUN_SEL(b, kern) CAND_SEL(b, kern)   // the persistent kernels: <U0Z, RL>
-// the low-occupancy phase kernel (k_nt_phase<..., LO = true>; never with X_CKPT)
+// the two-wavefront phase kernel (k_nt_phase<..., LO = true>; never with X_CKPT)
 #define PHASE_LO_SEL(b)                                                                                          \
     (((b)->flags & GYM_FLAG_REF_LANE)                                                                            \
          ? (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, true, true> : k_nt_phase<false, false, true, true>) \
@@ -3427,7 +3427,7 @@ static int device_cus() {
     return cache[dev];
 }
 
-// The phase kernel for a launch of `waves` wavefronts: the low-occupancy build (k_nt_phase<..., LO>) when the
+// The phase kernel for a launch of `waves` wavefronts: the two-wavefront build (k_nt_phase<..., LO>) when the
 // launch fills the SIMDs with between LO_MIN_EIGHTHS/8 and two wavefronts each (profiles/r06/README.md "pd2":
 // same-buffer A/B over batch sizes), the four-wavefront build otherwise.
 constexpr int LO_MIN_EIGHTHS = 14;

@@ -533,13 +533,13 @@ class BatchedNewtonSolver:
 
     def phase_kind(self) -> str | None:
         """The build of the phase kernel this batch's full phases launch (pipelined schedule; gym_newton_phase_kind):
-        "low-occupancy" (more than 7/8 and at most two wavefronts per SIMD: compiled for two, prefetching two stages
+        "two-wavefront" (more than 7/8 and at most two wavefronts per SIMD: compiled for two, prefetching two stages
         ahead) or "four-wavefront"; None for the other schedules.  Both builds give the same bits."""
         if self.schedule != "pipelined":
             return None
         lo = C.c_int32()
         _lib.check(self.eng.lib.gym_newton_phase_kind(C.byref(self.batch), C.byref(lo)), "gym_newton_phase_kind")
-        return "low-occupancy" if lo.value else "four-wavefront"
+        return "two-wavefront" if lo.value else "four-wavefront"
 
     # --- optional per-kernel HIP-event timing (on the solver's stream) ---------------------
     def enable_timing(self):

@@ -255,7 +255,7 @@ int gym_newton_pipeline_split(const gym_batch* bt, int64_t* Bh);
 int gym_newton_phase(const gym_model* m, const gym_weights* w, const gym_armijo* a, const gym_batch* bt, int32_t p,
                      int32_t do_backward, void* stream);
 /* Which build of the phase kernel gym_newton_phase launches for this batch's full phases on the current device:
- * *low_out = 1 for the low-occupancy build (more than 7/8 and at most two wavefronts per SIMD, no X_CKPT: compiled
+ * *low_out = 1 for the two-wavefront build (more than 7/8 and at most two wavefronts per SIMD, no X_CKPT: compiled
  * for two wavefronts, its stage loops prefetching two stages ahead), 0 for the four-wavefront build.  Both give the
  * same bits; this reports the choice (tests, the bench line).  ABI 17. */
 int gym_newton_phase_kind(const gym_batch* bt, int32_t* low_out);

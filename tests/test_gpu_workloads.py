@@ -95,12 +95,15 @@ def test_cfg4_rank_share_and_pooled_resolve():
     PlacementPool.clear()
 
 
-def test_low_occupancy_phase_kernel_is_bitwise_the_four_wavefront_one():
-    """gym_newton_phase picks its low-occupancy build (compiled for two wavefronts per SIMD, both stage loops
+def test_two_wavefront_phase_kernel_is_bitwise_the_four_wavefront_one():
+    """gym_newton_phase picks its two-wavefront build (compiled for two wavefronts per SIMD, both stage loops
     prefetching two stages ahead) for batches of more than 7/8 and at most two wavefronts per SIMD, e.g. the
     131,072 lanes of one rank's cfg 4 share, and its four-wavefront build for the headline 262,144.  Same arithmetic
-    in the same order: lanes [0, 131072) of the headline solve and the 131,072-lane solve agree bit for bit in every
-    output (iteration counts, statuses and rollouts on every lane; x, u, K, sigma and cost on every 97th lane)."""
+    in the same order: lanes [0, 131072) of a 262,144-lane solve and 131,072-lane solves on each instantiation of the
+    two-wavefront build (shared references with the tau1 planes skipped, the general kernels that stream them, and
+    per-lane references) agree bit for bit in every output: iteration counts, statuses and rollouts on every lane;
+    x, u, K, sigma and cost on every 97th lane.  Twice: the headline batch to convergence, and the stress start
+    (th ~ U(+-1.5): backtracking, the retry kernels after the phases) for 80 iterations."""
     import gc
     import torch
     from bench import load_refs, make_x0
@@ -109,24 +112,37 @@ def test_low_occupancy_phase_kernel_is_bitwise_the_four_wavefront_one():
     x_ref, u_ref = load_refs()
     eng = AcrobotEngine()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    x0 = make_x0(262144)
     kw = dict(tol=1e-4, beta=0.7, c=0.5, gamma_0=0.1, max_ls=20, placement_trials=1)
-    out = {}
-    for B in (131072, 262144):
-        s = BatchedNewtonSolver(eng, x_ref, u_ref, B, **kw)
+    H = 131072
+
+    def run(B, x0, iters, u0_zero=None, per_lane=False):
+        xr, ur = x_ref, u_ref
+        if per_lane:
+            xr = np.broadcast_to(x_ref, (B,) + x_ref.shape).copy()
+            ur = np.broadcast_to(u_ref, (B,) + u_ref.shape).copy()
+        s = BatchedNewtonSolver(eng, xr, ur, B, u0_zero=u0_zero, **kw)
         assert s.schedule == "pipelined"
         waves, simds = B // 64, 4 * cus
-        want = "low-occupancy" if 8 * waves > 14 * simds and waves <= 2 * simds else "four-wavefront"
+        want = "two-wavefront" if 8 * waves > 14 * simds and waves <= 2 * simds else "four-wavefront"
         assert s.phase_kind() == want, (B, cus, s.phase_kind())
-        if cus == 256:                           # MI355X: the rank share on the low-occupancy build, the headline not
-            assert want == ("low-occupancy" if B == 131072 else "four-wavefront")
-        r = s.solve(x0[:B], 5000, sync_every=4)
-        out[B] = {k: getattr(r, k)[:131072].cpu().numpy() for k in ("n_iter", "status", "n_rollouts")}
-        out[B].update({k: getattr(r, k)[:131072:97].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")})
+        if cus == 256:                           # MI355X: the rank share on the two-wavefront build, the headline not
+            assert want == ("two-wavefront" if B == H else "four-wavefront")
+        r = s.solve(x0[:B], iters, sync_every=4)
+        out = {k: getattr(r, k)[:H].cpu().numpy() for k in ("n_iter", "status", "n_rollouts")}
+        out.update({k: getattr(r, k)[:H:97].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")})
         del r, s
         gc.collect()
-    for k, v in out[262144].items():
-        assert np.array_equal(out[131072][k], v), k
+        return out
+
+    for spread, iters in ((0.5, 5000), (1.5, 80)):
+        x0 = make_x0(2 * H, spread=spread)
+        ref = run(2 * H, x0, iters)
+        if spread == 1.5:
+            assert (ref["n_rollouts"] > ref["n_iter"]).any()      # lanes backtracked
+        for case in (dict(), dict(u0_zero=False), dict(per_lane=True)):
+            got = run(H, x0, iters, **case)
+            for k, v in ref.items():
+                assert np.array_equal(got[k], v, equal_nan=True), (spread, case, k)
 
 
 def test_cfg4_global_batch_on_one_gpu():

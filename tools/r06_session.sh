@@ -81,7 +81,7 @@ for s in "$@"; do
     spread) for b in ${SP_BATCHES:-114688 131072 163840 196608 262144}; do
              GYM_ALLOW_FOREIGN_BUILD=1 step spread_ab_$b 400 python3 -u tools/ab_bench.py --batch $b --rounds 3 \
                build_ab/libA.so:pipe build_ab/libB.so:pipe build_ab/libC.so:pipe build_ab/libD.so:pipe || exit $?; done ;;
-    lotest) step pytest_lo 600 $PYT tests/test_gpu_workloads.py -m gpu -k "low_occupancy or rank_share" || exit $? ;;
+    lotest) step pytest_lo 600 $PYT tests/test_gpu_workloads.py -m gpu -k "two_wavefront or rank_share" || exit $? ;;
     sharebench) step bench_share 600 python3 -u bench.py --steps 5 --warmup 2 --no-cpu --extra-legs cfg4share,cfg4 \
                   || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
