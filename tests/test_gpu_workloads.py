@@ -103,7 +103,7 @@ def test_two_wavefront_phase_kernel_is_bitwise_the_four_wavefront_one():
     two-wavefront build (shared references with the tau1 planes skipped, the general kernels that stream them, and
     per-lane references) agree bit for bit in every output: iteration counts, statuses and rollouts on every lane;
     x, u, K, sigma and cost on every 97th lane.  Twice: the headline batch to convergence, and the stress start
-    (th ~ U(+-1.5): backtracking, the retry kernels after the phases) for 80 iterations."""
+    (th ~ U(+-1.5): backtracking, the retry kernels after the phases) for 150 iterations."""
     import gc
     import torch
     from bench import load_refs, make_x0
@@ -134,7 +134,7 @@ def test_two_wavefront_phase_kernel_is_bitwise_the_four_wavefront_one():
         gc.collect()
         return out
 
-    for spread, iters in ((0.5, 5000), (1.5, 80)):
+    for spread, iters in ((0.5, 5000), (1.5, 150)):
         x0 = make_x0(2 * H, spread=spread)
         ref = run(2 * H, x0, iters)
         if spread == 1.5:
