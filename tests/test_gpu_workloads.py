@@ -145,6 +145,37 @@ def test_two_wavefront_phase_kernel_is_bitwise_the_four_wavefront_one():
                 assert np.array_equal(got[k], v, equal_nan=True), (spread, case, k)
 
 
+@pytest.mark.parametrize("N", [202, 203, 4])
+def test_two_wavefront_phase_kernel_every_stage_remainder(N):
+    """The two-wavefront build's stage loops run three stages per trip and then the remaining T mod 3 (the headline's
+    T = 500 leaves 2): horizons T = 201, 202 and 3 (the reference trajectory cut to N knots) leave 0, 1 and 0 with a
+    single trip, and give bit for bit the four-wavefront build's results (lanes [0, 131072) of a 262,144-lane solve
+    against the 131,072-lane solve, 30 iterations; every lane's counts, every 97th lane's trajectories)."""
+    import gc
+    import torch
+    from bench import load_refs, make_x0
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    x_ref, u_ref = load_refs()
+    x_ref, u_ref = x_ref[:N].copy(), u_ref[:N - 1].copy()
+    eng = AcrobotEngine()
+    H = 131072
+    x0 = make_x0(2 * H)
+    out = []
+    for B in (2 * H, H):
+        s = BatchedNewtonSolver(eng, x_ref, u_ref, B, tol=1e-4, gamma_0=0.1, placement_trials=1, pipeline=True)
+        if torch.cuda.get_device_properties(0).multi_processor_count == 256:     # MI355X
+            assert s.phase_kind() == ("two-wavefront" if B == H else "four-wavefront")
+        r = s.solve(x0[:B], 30, sync_every=4)
+        o = {k: getattr(r, k)[:H].cpu().numpy() for k in ("n_iter", "status", "n_rollouts")}
+        o.update({k: getattr(r, k)[:H:97].cpu().numpy() for k in ("x", "u", "K", "sigma", "cost")})
+        out.append(o)
+        del r, s
+        gc.collect()
+    for k, v in out[0].items():
+        assert np.array_equal(out[1][k], v, equal_nan=True), (N, k)
+
+
 def test_cfg4_global_batch_on_one_gpu():
     """BASELINE cfg 4's whole batch, 1,048,576 lanes (bench.py's strong-scaling workload at N = 1; the pipelined
     schedule), solved to convergence on one GPU, checked through size-independent properties: every lane
