@@ -84,6 +84,9 @@ for s in "$@"; do
     lotest) step pytest_lo 600 $PYT tests/test_gpu_workloads.py -m gpu -k "two_wavefront or rank_share" || exit $? ;;
     sharebench) step bench_share 600 python3 -u bench.py --steps 5 --warmup 2 --no-cpu --extra-legs cfg4share,cfg4 \
                   || exit $? ;;
+    w3ab) for b in ${W3_BATCHES:-147456 163840 180224 196608}; do
+             GYM_ALLOW_FOREIGN_BUILD=1 step w3_ab_$b 400 python3 -u tools/ab_bench.py --batch $b --rounds 3 $LIB:pipe \
+               build_ab/libw3.so:pipe || exit $?; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
