@@ -87,6 +87,13 @@ for s in "$@"; do
     w3ab) for b in ${W3_BATCHES:-147456 163840 180224 196608}; do
              GYM_ALLOW_FOREIGN_BUILD=1 step w3_ab_$b 400 python3 -u tools/ab_bench.py --batch $b --rounds 3 $LIB:pipe \
                build_ab/libw3.so:pipe || exit $?; done ;;
+    pmc131) 
+            step pmc131_fetch 200 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_nt_phase" -d $OUT/pmc131_fetch -o run --output-format csv -- python3 -u bench.py --batch 131072 --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" && \
+            step pmc131_write 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_nt_phase" -d $OUT/pmc131_write -o run --output-format csv -- python3 -u bench.py --batch 131072 --steps 1 --warmup 0 --no-cpu --no-box --no-timing --max-iters 20 --extra-legs "" && \
+            step trace131 300 rocprofv3 --kernel-trace --stats -d $OUT/trace131 -o run --output-format csv -- python3 -u bench.py --batch 131072 --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" || exit $? ;;
+    curve) for b in ${CURVE_BATCHES:-16384 32768 65536 98304 131072 196608 262144 393216 524288 1048576}; do
+             step curve_$b 300 python3 -u bench.py --batch $b --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" \
+               || exit $?; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
