@@ -122,10 +122,12 @@ class BatchedNewtonSolver:
     # kernels crossed at ~81,920, profiles/r01_batch_sweep.log).  In lanes per compute unit (4 SIMDs x 64 x 2).
     PIPELINE_MIN_LANES_PER_CU = 512
     # The persistent schedule (one launch per solve: no per-iteration launches, statistics or host round trips)
-    # is ahead while the batch is latency-bound: its four-wavefront kernel (k_nt_run2) measured +59% over serial
-    # at 16,384 lanes, +10% at 24,576, +5.5% at 32,768 (= 2 workgroups per CU), and 10% behind from 36,864 on,
-    # where some CUs take a third workgroup (same box, profiles/r02_sched_sweep.log).
-    PERSISTENT_MAX_LANES_PER_CU = 128
+    # is ahead while the batch is latency-bound and fits in one round of its workgroups: k_nt_run2 holds 64 lanes
+    # on four wavefronts and ~98 KiB of LDS, one workgroup per CU.  Round 6, same box (profiles/r06/sched/):
+    # persistent 28.95 M it/s against serial 17.16 at 16,384 lanes (64 per CU), but 22.94 / 24.60 at 24,576 and
+    # 29.40 / 32.19 at 32,768, where CUs take a second workgroup (round 2's threshold of 128 per CU predates the
+    # kernel's LDS ring).
+    PERSISTENT_MAX_LANES_PER_CU = 64
     # The straggler tail (gym_newton_tail: one workgroup per lane, every Armijo trial at once) takes over the serial /
     # pipelined loop once at most this many lanes per CU (of all ranks) are still active: one wavefront per lane, so up
     # to one per SIMD it runs each lane's iteration at the latency of one sweep pass plus one trial chain.

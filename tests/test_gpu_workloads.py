@@ -345,12 +345,12 @@ def test_capture_lanes_reproduce_reference_history(schedule, task2_refs):
 
 
 # ------------------------------------------------------------------ sharded solve on the HIP path
-@pytest.mark.parametrize("total", [301, 65537])
+@pytest.mark.parametrize("total", [301, 32769])
 def test_sharded_solve_on_hip_matches_unsharded(total, tmp_path):
-    """Two ranks (gloo, sharing this GPU) run distributed.solve_sharded on the HIP solver.  65,537 lanes give
-    ragged shards of 32,769 / 32,768 lanes on either side of the persistent-schedule threshold (128 lanes per CU
+    """Two ranks (gloo, sharing this GPU) run distributed.solve_sharded on the HIP solver.  32,769 lanes give
+    ragged shards of 16,385 / 16,384 lanes on either side of the persistent-schedule threshold (64 lanes per CU
     on 256 CUs): both ranks must still pick the same schedule (chosen on the largest shard), pair up their
-    all-reduces, and reproduce the unsharded solve bit for bit; 301 lanes run the persistent schedule.  With 65,537
+    all-reduces, and reproduce the unsharded solve bit for bit; 301 lanes run the persistent schedule.  With 32,769
     lanes the worker also solves 2,000 hard lanes with lane compaction forced (rank-local) and the straggler tail
     (switched on the global count): gathered, the unsharded solve's bits."""
     import torch

@@ -94,6 +94,9 @@ for s in "$@"; do
     curve) for b in ${CURVE_BATCHES:-16384 32768 65536 98304 131072 196608 262144 393216 524288 1048576}; do
              step curve_$b 300 python3 -u bench.py --batch $b --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" \
                || exit $?; done ;;
+    sched) for b in ${SCHED_BATCHES:-16384 24576 32768 40960 49152}; do for sc in serial pipelined persistent; do
+             step sched_${b}_$sc 300 python3 -u bench.py --batch $b --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" \
+               --schedule $sc || exit $?; done; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
