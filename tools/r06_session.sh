@@ -97,6 +97,9 @@ for s in "$@"; do
     sched) for b in ${SCHED_BATCHES:-16384 24576 32768 40960 49152}; do for sc in serial pipelined persistent; do
              step sched_${b}_$sc 300 python3 -u bench.py --batch $b --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" \
                --schedule $sc || exit $?; done; done ;;
+    small) for b in 16384 24576 32768; do
+             step small_$b 300 python3 -u bench.py --batch $b --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" \
+               || exit $?; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
