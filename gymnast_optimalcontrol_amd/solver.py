@@ -599,6 +599,7 @@ class BatchedNewtonSolver:
         self._capture_start(self.capture_lanes or [])
         self._serial_now = False   # the low-occupancy regime (maybe_compact / _enter_low_occupancy)
         self._run_now = False
+        self._sigma_streamed = False
         self.batch.flags &= ~_lib.FLAG_SIGMA_STREAM
         if self.pipeline and not self.persistent and (self.max_iters is None or self.max_iters > 0):
             self._phase(0, True)                 # prologue: backward sweep of half H0, iteration 0
@@ -772,8 +773,27 @@ class BatchedNewtonSolver:
         """u (B,T,2) of control buffer ``buf``."""
         return self.eng.unpack(self.u[buf], self.B)
 
-    def sigma(self) -> torch.Tensor:
-        """sigma (B,T,2) of every lane's last completed iteration (its sweep re-run: sigma1 is not streamed)."""
+    def stream_sigma(self):
+        """Call right after init(): run every iteration as the low-occupancy regime does (one launch of the
+        four-wavefront persistent kernel per iteration, its sweep storing sigma1; _enter_low_occupancy), so that
+        sigma() reads each iteration's sigma from the stored plane instead of re-running every lane's sweep.  For
+        callers that want every iteration's sigma of a few lanes (the drop-in newton_Algorithm's history).  The same
+        bits as any schedule."""
+        if self.k != 0:
+            raise RuntimeError("stream_sigma() must follow init() directly")
+        self.pipeline = False
+        self._enter_low_occupancy()
+        self._sigma_streamed = True
+        return self
+
+    def sigma(self, rerun: bool = False) -> torch.Tensor:
+        """sigma (B,T,2) of every lane's last completed iteration: its sweep re-run (sigma1 is not streamed), or,
+        after stream_sigma() with the tau1 channel zero (u0_zero: sigma0 = -(2R0 (u0 - ur0)) / (2R0) = -0 on every
+        stage), the sigma1 plane that iteration's sweep stored -- bit for bit the re-run (``rerun`` forces it)."""
+        if self._sigma_streamed and self.u0_zero and not rerun:
+            s = self.eng.unpack(self.cs, self.B)      # (B, T, 2): cg, sigma1
+            s[..., 0] = -0.0
+            return s
         s = torch.empty((self.B, self.T, 2), dtype=F64, device=self.eng.device)
         _lib.check(self.eng.lib.gym_newton_sigma(C.byref(self.eng.model), C.byref(self.eng._w), C.byref(self.batch),
                                                  s.data_ptr(),

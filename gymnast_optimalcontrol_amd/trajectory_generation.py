@@ -346,6 +346,7 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
                                  max_ls=MAX_LINE_SEARCH_ITERS, pipeline=False)
     x0 = np.asarray(x0, dtype=float).reshape(1, 4)
     solver.init(x0)
+    solver.stream_sigma()   # one four-wavefront launch per iteration, sigma1 stored by its sweep (the same bits)
     Tn = x_ref.shape[0] - 1
 
     def lane_x(buf):

@@ -185,6 +185,45 @@ def test_task2_newton_algorithm_matches_reference_golden(tg, golden, task2_refs)
         np.testing.assert_allclose(hist["x_trajs"][i], run["x_hist"][j], rtol=1e-9, atol=1e-12)
 
 
+def test_streamed_sigma_is_the_rerun_bit_for_bit(task2_refs):
+    """The drop-in newton_Algorithm runs its solver with stream_sigma(): one four-wavefront persistent launch per
+    iteration whose sweep stores sigma1, read back by sigma() instead of re-running the sweep.  After every
+    iteration that sigma equals the re-run's bit for bit (sign of zero included), and the iterates, costs and
+    decisions equal the serial schedule's, on lanes that converge, backtrack and fail the line search."""
+    import torch
+    from gymnast_optimalcontrol_amd.engine import AcrobotEngine
+    from gymnast_optimalcontrol_amd.solver import BatchedNewtonSolver
+    xr, ur, _ = task2_refs
+    x0 = np.zeros((6, 4))
+    x0[1, :2] = [1.2, -1.3]
+    x0[2, :2] = [2.9, -2.5]
+    x0[3, :2] = [0.3, 0.2]
+    x0[4, :2] = [-1.4, 1.45]
+    x0[5] = np.nan
+    eng = AcrobotEngine()
+    kw = dict(tol=1e-4, gamma_0=0.1, pipeline=False)
+    a = BatchedNewtonSolver(eng, xr, ur, 6, **kw)
+    b = BatchedNewtonSolver(eng, xr, ur, 6, **kw)
+    a.init(x0)
+    a.stream_sigma()
+    b.init(x0)
+    seen_backtrack = False
+    for k in range(120):
+        a.iteration()
+        b.iteration()
+        fast, rerun = a.sigma(), a.sigma(rerun=True)
+        assert torch.equal(fast.view(torch.int64), rerun.view(torch.int64)), k
+        assert torch.equal(fast.view(torch.int64), b.sigma().view(torch.int64)), k
+        for name in ("cost", "status", "n_iter", "n_roll", "gamma", "smax"):
+            va, vb = getattr(a, name)[:6], getattr(b, name)[:6]
+            assert torch.equal(va.view(torch.int64) if va.is_floating_point() else va,
+                               vb.view(torch.int64) if vb.is_floating_point() else vb), (k, name)
+        seen_backtrack |= bool((a.n_roll[:6] > a.n_iter[:6]).any())
+    assert seen_backtrack
+    for ta, tb in zip(a.finalize(), b.finalize()):      # every lane's result iterate, controls, gains, sigma
+        assert torch.equal(ta.view(torch.int64), tb.view(torch.int64))
+
+
 def test_task1_with_live_tau1_channel(tg, golden):
     g = golden("task1_solve")
     x, u, K, sigma, hist = tg.newton_Algorithm(g["x0"], g["x_ref"], g["u_ref_full"], max_iters=5000, tol=1e-4,

@@ -100,6 +100,16 @@ for s in "$@"; do
     small) for b in 16384 24576 32768; do
              step small_$b 300 python3 -u bench.py --batch $b --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" \
                || exit $?; done ;;
+    mid) for b in ${MID_BATCHES:-98304 114688 118784 122880 126976}; do for sc in serial pipelined; do
+             step mid_${b}_$sc 300 python3 -u bench.py --batch $b --steps 3 --warmup 1 --no-cpu --no-box --extra-legs "" \
+               --schedule $sc || exit $?; done; done ;;
+    cfg1prof) step cfg1_cprofile 300 python3 -u tools/cfg1_profile.py --cprofile $OUT/cfg1_cprofile.txt && \
+              step cfg1_trace 300 rocprofv3 --kernel-trace --stats -d $OUT/cfg1_trace -o run --output-format csv -- \
+                python3 -u tools/cfg1_profile.py || exit $? ;;
+    sigtest) step pytest_sig 600 $PYT tests/test_gpu_parity.py tests/test_armijo_sweep.py tests/test_report.py \
+               -m gpu -k "streamed_sigma or task2 or task1 or batched_lanes or armijo or reference_history or report" \
+               && step pytest_sig2 600 $PYT tests/test_gpu_workloads.py -m gpu -k "capture_lanes" || exit $? ;;
+    cfg1) step cfg1_time 300 python3 -u tools/cfg1_profile.py || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
