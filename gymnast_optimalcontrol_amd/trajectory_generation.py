@@ -352,9 +352,6 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
     def lane_x(buf):
         return eng.unpack(solver.states(buf), 1)[0].cpu().numpy()
 
-    def lane_sigma():
-        return solver.sigma()[0].cpu().numpy()
-
     x_traj = lane_x(0)
     assert x_traj.shape[0] == x_ref.shape[0], \
         f"Simulated trajectory length mismatch: {x_traj.shape[0]} vs {x_ref.shape[0]}"
@@ -369,10 +366,14 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
             x_prev, u_prev = history["x_trajs"][-1], solver.controls(k & 1)[0].cpu().numpy()
             rolls = int(solver.n_roll[0].item())
         solver.iteration()
-        status = int(solver.status[0].item())
-        sig = lane_sigma()
+        # one device -> host copy per iteration: status, max|sigma|, cost, sigma (T,2) and the new iterate (N,4)
+        rec = torch.cat([solver.status[:1].to(torch.float64), solver.smax[:1], solver.cost[:1],
+                         solver.sigma()[0].reshape(-1),
+                         eng.unpack(solver.states(solver.k & 1), 1)[0].reshape(-1)]).cpu().numpy()
+        status = int(rec[0])
+        sig = rec[3:3 + 2 * Tn].reshape(Tn, 2)
         history["sigmas"].append(list(sig))          # row views of this iteration's own (T,2) array
-        history["sigma_norm"].append(float(solver.smax[0].item()))
+        history["sigma_norm"].append(float(rec[1]))
         if status == _lib.LS_FAILED:
             if verbose:
                 print(f"Iteration {k}: Line search failed to find sufficient decrease.")
@@ -384,9 +385,9 @@ def newton_Algorithm(x0, x_ref, u_ref, max_iters, tol=1e-6, beta=0.7, c=0.5, gam
                                     prev_cost, x_ref, u_ref, float(solver.dJ[0].item()),
                                     float(solver.gamma[0].item()), list(trial_gammas[:n_tested]),
                                     list(trial_costs[:n_tested]), c, beta)
-        cost_k = float(solver.cost[0].item())
+        cost_k = float(rec[2])
         history["cost"].append(cost_k)
-        history["x_trajs"].append(lane_x(solver.k & 1))
+        history["x_trajs"].append(rec[3 + 2 * Tn:].reshape(-1, 4))
         if verbose and k % 10 == 0:
             print(f"Iter {k}: Cost={cost_k:.2f}, diff_cost={prev_cost - cost_k:.2e}, ")
         if status == _lib.CONVERGED:
