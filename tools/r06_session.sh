@@ -110,6 +110,9 @@ for s in "$@"; do
                -m gpu -k "streamed_sigma or task2 or task1 or batched_lanes or armijo or reference_history or report" \
                && step pytest_sig2 600 $PYT tests/test_gpu_workloads.py -m gpu -k "capture_lanes" || exit $? ;;
     cfg1) step cfg1_time 300 python3 -u tools/cfg1_profile.py || exit $? ;;
+    tailsw) for tl in ${TAIL_SET:-1024 2048 512}; do
+             step tail_$tl 300 python3 -u bench.py --workload stress --steps 2 --warmup 1 --no-cpu --no-box --extra-legs "" \
+               --tail-lanes $tl || exit $?; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
