@@ -1490,9 +1490,8 @@ __global__ __launch_bounds__(BLK, LO ? 2 : 4) void k_nt_phase(PhaseArgs args) {
                 backward_solver_lane_ck<U0Z, OUT_SOLVER>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1, R->cs,
                                                          R->a.gamma0, ck_lds, l, R->Bp, R->N, d, s);
             else
-                backward_solver_lane<U0Z, OUT_SOLVER, true, PD>(R->m, R->w, R->xb_in, R->ub_in, xr, ur,
-                                                                         R->K1, R->cs, R->a.gamma0, l, R->Bp, R->N,
-                                                                         d, s);
+                backward_solver_lane<U0Z, OUT_SOLVER, true, PD>(R->m, R->w, R->xb_in, R->ub_in, xr, ur, R->K1,
+                                                                R->cs, R->a.gamma0, l, R->Bp, R->N, d, s);
         }
         const pargs_t Q = phase_args();
         Q->dJ[l] = d;
@@ -1505,11 +1504,10 @@ __global__ __launch_bounds__(BLK, LO ? 2 : 4) void k_nt_phase(PhaseArgs args) {
         {   // Armijo trial 1 (gamma0) fused with the candidate rollout and its cost (:352-365, first pass)
             const pargs_t R = phase_args();
             const double2 xa = R->io.x[wix(0, 0, 2, l, R->Bp)], xb = R->io.x[wix(0, 1, 2, l, R->Bp)];
-            Jn = rollout_cform<true, U0Z, false, CK, kNT, true, PD>(R->m, R->w, R->io.u, R->K1, R->cs,
-                                                     lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N),
-                                                     lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1)), R->io.xn,
-                                                     R->io.un, R->a.gamma0, R->a.gamma0, l, R->Bp, R->N, xa.x, xa.y,
-                                                     xb.x, xb.y);
+            Jn = rollout_cform<true, U0Z, false, CK, kNT, true, PD>(
+                R->m, R->w, R->io.u, R->K1, R->cs, lane_ref<RL>(R->xr, l, 4 * (int64_t)R->N),
+                lane_ref<RL>(R->ur, l, 2 * (int64_t)(R->N - 1)), R->io.xn, R->io.un, R->a.gamma0, R->a.gamma0, l,
+                R->Bp, R->N, xa.x, xa.y, xb.x, xb.y);
         }
         const pargs_t R = phase_args();
         const SolverCtl a = R->a;
@@ -1747,9 +1745,9 @@ __global__ __launch_bounds__(BLK) void k_nt_retry(Dyn m, KW w, SolverCtl a, Tria
 // or host round trip per iteration.  Per lane the arithmetic is the other schedules' (same device functions):
 // bit-identical results.  No wave priority bands (measured: the phase kernels' per-pass bands 4-8% slower here,
 // each pass restarting at priority 3 undoes them; cyclic bands of the iteration count no faster than none).
-// The kernel serves batches of at most 128 lanes per CU, i.e. at most one wavefront per SIMD, so it is compiled for
-// one (__launch_bounds__(BLK, 1)), and its sweep interleaves stage t-1's Jacobian with stage t's Riccati update
-// (backward_solver_lane_ilp).
+// The kernel serves batches of at most 128 lanes per CU (the solver's default: 64), i.e. at most one wavefront per
+// SIMD, so it is compiled for one (__launch_bounds__(BLK, 1)), and its sweep interleaves stage t-1's Jacobian with
+// stage t's Riccati update (backward_solver_lane_ilp).
 // ------------------------------------------------------------------------------------------
 // Everything the kernel needs beyond the stage loops' own operands is one by-value struct whose fields are
 // re-read from the kernel-argument segment at each use (run_args(): scalar loads behind an opaque pointer),
@@ -3112,10 +3110,10 @@ struct TimedLaunch {  // records a start/stop event pair around one launch: a po
 #define RUN_SEL(b, kern) CAND_SEL(b, kern)   // the persistent kernels: <U0Z, RL>
 // the two-wavefront phase kernel (k_nt_phase<..., LO = true>; never with X_CKPT)
 #define PHASE_LO_SEL(b)                                                                                          \
-    (((b)->flags & GYM_FLAG_REF_LANE)                                                                            \
-         ? (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, true, true> : k_nt_phase<false, false, true, true>) \
-         : (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, false, true>                               \
-                                             : k_nt_phase<false, false, false, true>))
+    (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, true, true>  \
+                                                                          : k_nt_phase<false, false, true, true>) \
+                                      : (((b)->flags & GYM_FLAG_U0_ZERO) ? k_nt_phase<true, false, false, true> \
+                                                                          : k_nt_phase<false, false, false, true>))
 #define CAND_SEL(b, kern)                                                                                        \
     (((b)->flags & GYM_FLAG_REF_LANE) ? (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, true> : kern<false, true>) \
                                       : (((b)->flags & GYM_FLAG_U0_ZERO) ? kern<true, false> : kern<false, false>))
